@@ -1,0 +1,311 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY. Never linked into the product.
+// CPU statement of armour-IPM (see ipm.h). The GPU solver (armour-dev_amd/csrc/nlp_kernels.hip)
+// implements the same passes; reductions there run in a different order, so iterates agree to
+// rounding, not bit for bit.
+#include "ipm.h"
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+#include <cstdio>
+#include <cstdlib>
+
+namespace oracle {
+
+static const int NMAX = 8;
+
+// Cholesky of a dense n x n SPD matrix (row-major) with diagonal shift; returns false if not PD
+static bool chol_solve(const double* M, int n, double shift, const double* b, double* x) {
+    double L[NMAX * NMAX];
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j <= i; j++) {
+            double s = M[i * n + j] + (i == j ? shift : 0.0);
+            for (int k = 0; k < j; k++) s -= L[i * n + k] * L[j * n + k];
+            if (i == j) {
+                if (!(s > 0)) return false;
+                L[i * n + i] = std::sqrt(s);
+            } else {
+                L[i * n + j] = s / L[j * n + j];
+            }
+        }
+    double y[NMAX];
+    for (int i = 0; i < n; i++) {
+        double s = b[i];
+        for (int k = 0; k < i; k++) s -= L[i * n + k] * y[k];
+        y[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double s = y[i];
+        for (int k = i + 1; k < n; k++) s -= L[k * n + i] * x[k];
+        x[i] = s / L[i * n + i];
+    }
+    return true;
+}
+
+IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* g_out) {
+    const int n = prob.n(), m = prob.m();
+    const int R = m + n;  // constraint rows + box rows
+    std::vector<double> L(R), U(R);
+    {
+        std::vector<double> xl(n), xu(n), gl(m), gu(m);
+        prob.bounds(xl.data(), xu.data(), gl.data(), gu.data());
+        for (int r = 0; r < m; r++) { L[r] = gl[r]; U[r] = gu[r]; }
+        for (int j = 0; j < n; j++) { L[m + j] = xl[j]; U[m + j] = xu[j]; }
+        // Ipopt-style push of the start point into the box interior
+        for (int j = 0; j < n; j++) {
+            const double p = std::min(opt.bound_push * std::max(1.0, std::fabs(xl[j])), opt.bound_push * (xu[j] - xl[j]));
+            x[j] = std::min(std::max(x[j], xl[j] + p), xu[j] - p);
+        }
+    }
+    std::vector<char> hlo(R), hhi(R);
+    for (int r = 0; r < R; r++) { hlo[r] = L[r] > -opt.inf_bound; hhi[r] = U[r] < opt.inf_bound; }
+
+    // evaluation buffers (current and trial)
+    std::vector<double> g(m), J((size_t)m * n), gt(m), Jt((size_t)m * n);
+    double f, ft, grad[NMAX], gradt[NMAX];
+    prob.eval(x, &f, grad, g.data(), J.data());
+    int nevals = 1;
+
+    auto val = [&](const std::vector<double>& gv, const double* xv, int r) { return r < m ? gv[r] : xv[r - m]; };
+    auto grow = [&](const std::vector<double>& Jv, int r, double* a) {
+        if (r < m) for (int j = 0; j < n; j++) a[j] = Jv[(size_t)r * n + j];
+        else for (int j = 0; j < n; j++) a[j] = (j == r - m) ? 1.0 : 0.0;
+    };
+
+    std::vector<double> slo(R, 0), shi(R, 0), zlo(R, 0), zhi(R, 0);
+    std::vector<double> dslo(R, 0), dshi(R, 0), dzlo(R, 0), dzhi(R, 0), rplo(R, 0), rphi(R, 0);
+    double mu = opt.mu0;
+    for (int r = 0; r < R; r++) {
+        const double v = val(g, x, r);
+        double p = 0;
+        if (hlo[r] && hhi[r]) p = std::min(opt.bound_push * std::max(1.0, std::fabs(L[r])), opt.bound_push * (U[r] - L[r]));
+        if (hlo[r]) {
+            const double pl = hhi[r] ? p : opt.bound_push * std::max(1.0, std::fabs(L[r]));
+            slo[r] = std::max(v - L[r], pl);
+            zlo[r] = mu / slo[r];
+        }
+        if (hhi[r]) {
+            const double pu = hlo[r] ? p : opt.bound_push * std::max(1.0, std::fabs(U[r]));
+            shi[r] = std::max(U[r] - v, pu);
+            zhi[r] = mu / shi[r];
+        }
+    }
+
+    double H[NMAX * NMAX] = {0};
+    for (int j = 0; j < n; j++) H[j * n + j] = 1.0;
+    bool first_update = true;
+    std::vector<double> filt_theta, filt_phi;
+    double theta_max = -1, theta_min = -1;
+    int nfail = 0;
+    IpmResult res{1, 0, 0, 0.0, 0.0};
+    double a[NMAX], at[NMAX];
+    int it;
+    for (it = 0; it < opt.max_iter; it++) {
+        // 1. residuals and errors
+        double rd[NMAX];
+        for (int j = 0; j < n; j++) rd[j] = grad[j];
+        double inf_p = 0, compl0 = 0, sumz = 0;
+        int nside = 0;
+        for (int r = 0; r < R; r++) {
+            const double v = val(g, x, r);
+            grow(J, r, a);
+            double w = 0;
+            if (hlo[r]) {
+                rplo[r] = (v - L[r]) - slo[r];
+                w += zlo[r];
+                inf_p = std::max(inf_p, std::fabs(rplo[r]));
+                compl0 = std::max(compl0, slo[r] * zlo[r]);
+                sumz += zlo[r];
+                nside++;
+            }
+            if (hhi[r]) {
+                rphi[r] = (U[r] - v) - shi[r];
+                w -= zhi[r];
+                inf_p = std::max(inf_p, std::fabs(rphi[r]));
+                compl0 = std::max(compl0, shi[r] * zhi[r]);
+                sumz += zhi[r];
+                nside++;
+            }
+            for (int j = 0; j < n; j++) rd[j] -= w * a[j];
+        }
+        double inf_d = 0;
+        for (int j = 0; j < n; j++) inf_d = std::max(inf_d, std::fabs(rd[j]));
+        const double sd = std::max(opt.s_max, sumz / std::max(1, nside)) / opt.s_max;
+        const double E0 = std::max(std::max(inf_d / sd, inf_p), compl0 / sd);
+        res.kkt_error = E0;
+        if (E0 <= opt.tol) { res.status = 0; break; }
+        // 2. monotone barrier update (at most one decrease per iteration)
+        {
+            double cm = 0;
+            for (int r = 0; r < R; r++) {
+                if (hlo[r]) cm = std::max(cm, std::fabs(slo[r] * zlo[r] - mu));
+                if (hhi[r]) cm = std::max(cm, std::fabs(shi[r] * zhi[r] - mu));
+            }
+            const double Emu = std::max(std::max(inf_d / sd, inf_p), cm / sd);
+            if (Emu <= opt.kappa_eps * mu && mu > opt.tol / 10) {
+                mu = std::max(opt.tol / 10, std::min(opt.kappa_mu * mu, std::pow(mu, opt.theta_mu)));
+                filt_theta.clear();
+                filt_phi.clear();
+            }
+        }
+        // 3. reduced Newton system
+        double M[NMAX * NMAX], rhs[NMAX];
+        for (int i = 0; i < n * n; i++) M[i] = H[i];
+        for (int j = 0; j < n; j++) rhs[j] = -grad[j];
+        for (int r = 0; r < R; r++) {
+            grow(J, r, a);
+            double sig = 0, c = 0;
+            if (hlo[r]) { const double s = zlo[r] / slo[r]; sig += s; c += mu / slo[r] - s * rplo[r]; }
+            if (hhi[r]) { const double s = zhi[r] / shi[r]; sig += s; c -= mu / shi[r] - s * rphi[r]; }
+            for (int i = 0; i < n; i++) {
+                rhs[i] += a[i] * c;
+                for (int j = 0; j < n; j++) M[i * n + j] += sig * a[i] * a[j];
+            }
+        }
+        double dx[NMAX];
+        {
+            double shift = 0.0;
+            while (!chol_solve(M, n, shift, rhs, dx)) shift = (shift == 0.0) ? 1e-8 : shift * 10;
+        }
+        // 4. step components and fraction to boundary
+        const double tau = std::max(opt.tau_min, 1.0 - mu);
+        double ap = 1.0, ad = 1.0, rp1 = 0, bdir = 0, logs = 0;
+        for (int r = 0; r < R; r++) {
+            grow(J, r, a);
+            double adx = 0;
+            for (int j = 0; j < n; j++) adx += a[j] * dx[j];
+            if (hlo[r]) {
+                const double s = zlo[r] / slo[r];
+                dslo[r] = adx + rplo[r];
+                dzlo[r] = mu / slo[r] - zlo[r] - s * dslo[r];
+                if (dslo[r] < 0) ap = std::min(ap, -tau * slo[r] / dslo[r]);
+                if (dzlo[r] < 0) ad = std::min(ad, -tau * zlo[r] / dzlo[r]);
+                rp1 += std::fabs(rplo[r]); bdir += dslo[r] / slo[r]; logs += std::log(slo[r]);
+            }
+            if (hhi[r]) {
+                const double s = zhi[r] / shi[r];
+                dshi[r] = -adx + rphi[r];
+                dzhi[r] = mu / shi[r] - zhi[r] - s * dshi[r];
+                if (dshi[r] < 0) ap = std::min(ap, -tau * shi[r] / dshi[r]);
+                if (dzhi[r] < 0) ad = std::min(ad, -tau * zhi[r] / dzhi[r]);
+                rp1 += std::fabs(rphi[r]); bdir += dshi[r] / shi[r]; logs += std::log(shi[r]);
+            }
+        }
+        // 5. filter line search (Ipopt's, without restoration): theta = ||c(x) - s||_1,
+        //    barrier objective phi = f - mu sum ln s
+        double gdx = 0;
+        for (int i = 0; i < n; i++) gdx += grad[i] * dx[i];
+        const double theta0 = rp1;
+        if (theta_min < 0) theta_min = 1e-4 * std::max(1.0, theta0);
+        const double phi0 = f - mu * logs;
+        const double Dphi = gdx - mu * bdir;
+        if (theta_max < 0) theta_max = 1e4 * std::max(1.0, theta0);
+        // BFGS needs sum_r w_r a_r(x) with the updated multipliers z + ad*dz
+        double wa_old[NMAX] = {0};
+        for (int r = 0; r < R; r++) {
+            double w = 0;
+            if (hlo[r]) w += zlo[r] + ad * dzlo[r];
+            if (hhi[r]) w -= zhi[r] + ad * dzhi[r];
+            grow(J, r, a);
+            for (int j = 0; j < n; j++) wa_old[j] += w * a[j];
+        }
+        double alpha = ap, xt[NMAX];
+        bool accepted = false, ftype = false;
+        for (int ls = 0; ls < opt.max_ls; ls++) {
+            for (int j = 0; j < n; j++) xt[j] = x[j] + alpha * dx[j];
+            prob.eval(xt, &ft, gradt, gt.data(), Jt.data());
+            nevals++;
+            double logt = 0, rpt = 0;
+            for (int r = 0; r < R; r++) {
+                const double v = val(gt, xt, r);
+                if (hlo[r]) { const double st = slo[r] + alpha * dslo[r]; logt += std::log(st); rpt += std::fabs((v - L[r]) - st); }
+                if (hhi[r]) { const double st = shi[r] + alpha * dshi[r]; logt += std::log(st); rpt += std::fabs((U[r] - v) - st); }
+            }
+            const double phit = ft - mu * logt, thetat = rpt;
+            bool ok = thetat <= theta_max;
+            for (size_t q = 0; ok && q < filt_theta.size(); q++)
+                if (!(thetat < filt_theta[q] || phit < filt_phi[q])) ok = false;
+            if (ok) {
+                const bool switching = Dphi < 0 && alpha * std::pow(-Dphi, 2.3) > std::pow(theta0, 1.1);
+                if (switching && theta0 <= theta_min) {
+                    ok = phit <= phi0 + opt.eta * alpha * Dphi;
+                    ftype = ok;
+                } else {
+                    ok = thetat <= (1 - 1e-5) * theta0 || phit <= phi0 - 1e-8 * theta0;
+                    if (!ok && switching) { ok = phit <= phi0 + opt.eta * alpha * Dphi; ftype = ok; }
+                }
+            }
+            if (ok) { accepted = true; break; }
+            if (ls + 1 < opt.max_ls) alpha *= 0.5;
+        }
+        if (accepted && !ftype) { filt_theta.push_back((1 - 1e-5) * theta0); filt_phi.push_back(phi0 - 1e-8 * theta0); }
+        const double nu = 0, D = Dphi, f_dbg = f; (void)f_dbg;
+        nfail = accepted ? 0 : nfail + 1;
+        if (getenv("IPM_DEBUG")) fprintf(stderr, "it %d mu %.2e E0 %.3e infd %.2e infp %.2e c0 %.2e ap %.3e ad %.3e alpha %.3e acc %d nu %.2e f %.5f rp1 %.3e D %.3e |dx| %.3e\n", it, mu, E0, inf_d, inf_p, compl0, ap, ad, alpha, (int)accepted, nu, f, rp1, D, std::sqrt(dx[0]*dx[0]+dx[1]*dx[1]+dx[2]*dx[2]+dx[3]*dx[3]+dx[4]*dx[4]+dx[5]*dx[5]+dx[6]*dx[6]));
+        // 6. accept the trial point; multipliers with kappa_sigma safeguard
+        double wa_new[NMAX] = {0};
+        for (int r = 0; r < R; r++) {
+            double w = 0;
+            if (hlo[r]) {
+                const double zn = zlo[r] + ad * dzlo[r];
+                w += zn;
+                slo[r] = slo[r] + alpha * dslo[r];
+                zlo[r] = std::min(std::max(zn, mu / (opt.kappa_sigma * slo[r])), opt.kappa_sigma * mu / slo[r]);
+            }
+            if (hhi[r]) {
+                const double zn = zhi[r] + ad * dzhi[r];
+                w -= zn;
+                shi[r] = shi[r] + alpha * dshi[r];
+                zhi[r] = std::min(std::max(zn, mu / (opt.kappa_sigma * shi[r])), opt.kappa_sigma * mu / shi[r]);
+            }
+            grow(Jt, r, at);
+            for (int j = 0; j < n; j++) wa_new[j] += w * at[j];
+        }
+        // damped BFGS on the Lagrangian Hessian
+        {
+            double sv[NMAX], y[NMAX], Hs[NMAX];
+            double ss = 0;
+            for (int j = 0; j < n; j++) {
+                sv[j] = xt[j] - x[j];
+                y[j] = (gradt[j] - grad[j]) - (wa_new[j] - wa_old[j]);
+                ss += sv[j] * sv[j];
+            }
+            double sy = 0;
+            for (int j = 0; j < n; j++) sy += sv[j] * y[j];
+            if (first_update && sy > 0 && ss > 1e-20) {
+                double yy = 0;
+                for (int j = 0; j < n; j++) yy += y[j] * y[j];
+                const double sc = yy / sy;
+                for (int i = 0; i < n * n; i++) H[i] = 0;
+                for (int j = 0; j < n; j++) H[j * n + j] = sc;
+                first_update = false;
+            }
+            double sHs = 0;
+            for (int i = 0; i < n; i++) {
+                Hs[i] = 0;
+                for (int j = 0; j < n; j++) Hs[i] += H[i * n + j] * sv[j];
+                sHs += sv[i] * Hs[i];
+            }
+            if (ss > 1e-20 && sHs > 1e-20) {
+                const double theta = (sy >= 0.2 * sHs) ? 1.0 : 0.8 * sHs / (sHs - sy);
+                double rv[NMAX], sr = 0;
+                for (int j = 0; j < n; j++) { rv[j] = theta * y[j] + (1 - theta) * Hs[j]; sr += sv[j] * rv[j]; }
+                if (sr > 1e-20)
+                    for (int i = 0; i < n; i++)
+                        for (int j = 0; j < n; j++) H[i * n + j] += -Hs[i] * Hs[j] / sHs + rv[i] * rv[j] / sr;
+            }
+        }
+        for (int j = 0; j < n; j++) { x[j] = xt[j]; grad[j] = gradt[j]; }
+        f = ft;
+        g.swap(gt);
+        J.swap(Jt);
+        if (nfail >= 3) { res.status = 2; it++; break; }
+    }
+    res.iterations = it;
+    res.evaluations = nevals;
+    res.obj = f;
+    std::memcpy(g_out, g.data(), sizeof(double) * m);
+    return res;
+}
+
+}  // namespace oracle
