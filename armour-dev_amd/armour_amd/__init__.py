@@ -1,0 +1,173 @@
+"""armour_amd — Python binding of the MI355X-native ARMOUR planner (libarmour_hip.so).
+
+The product is the C ABI in include/armour_hip.h; this module is a thin ctypes layer over it,
+used by tests/, bench.py and __graft_entry__.py. It loads the in-tree library and raises if the
+library or a GPU is missing — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .robots import KINOVA
+from .worlds import example_world, make_world
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libarmour_hip.so")
+NF = 7
+_LIB = None
+_dp = ctypes.POINTER(ctypes.c_double)
+
+
+class ArmourError(RuntimeError):
+    pass
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("robot", ctypes.c_int), ("num_time_steps", ctypes.c_int), ("max_obstacles", ctypes.c_int),
+                ("max_worlds", ctypes.c_int), ("device", ctypes.c_int), ("max_iter", ctypes.c_int)]
+
+
+class World(ctypes.Structure):
+    _fields_ = [("q0", ctypes.c_double * NF), ("qd0", ctypes.c_double * NF), ("qdd0", ctypes.c_double * NF),
+                ("q_des", ctypes.c_double * NF), ("num_obstacles", ctypes.c_int), ("obstacles", _dp)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("k_opt", ctypes.c_double * NF), ("feasible", ctypes.c_int), ("solver_status", ctypes.c_int),
+                ("iterations", ctypes.c_int), ("evaluations", ctypes.c_int), ("cost", ctypes.c_double),
+                ("kkt_error", ctypes.c_double)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("reach_ms", ctypes.c_double), ("nlp_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ArmourError(f"HIP planner library not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.armour_create.restype = ctypes.c_void_p
+        L.armour_create.argtypes = [ctypes.POINTER(Config)]
+        L.armour_destroy.argtypes = [ctypes.c_void_p]
+        L.armour_last_error.restype = ctypes.c_char_p
+        L.armour_num_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.armour_num_joints.argtypes = [ctypes.c_void_p]
+        L.armour_plan_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Result),
+                                        ctypes.POINTER(Timing)]
+        L.armour_reach_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Timing)]
+        L.armour_eval_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
+        for name in ("armour_get_constraints", "armour_get_link_centers", "armour_get_link_generators",
+                     "armour_get_torque_radius"):
+            getattr(L, name).argtypes = [ctypes.c_void_p, ctypes.c_int, _dp]
+        _LIB = L
+    return _LIB
+
+
+# every symbol include/armour_hip.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = ["armour_create", "armour_destroy", "armour_last_error", "armour_num_constraints",
+               "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
+               "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
+               "armour_num_joints"]
+
+
+def _check(rc):
+    if rc != 0:
+        raise ArmourError(f"armour error {rc}: {lib().armour_last_error().decode()}")
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_dp) if a is not None else None
+
+
+class Planner:
+    """Batched MI355X planner. A world is (q0, qd0, qdd0, q_des, obstacles[O, 12])."""
+
+    def __init__(self, T=100, max_obstacles=20, max_worlds=1, device=0, max_iter=0):
+        cfg = Config(0, T, max_obstacles, max_worlds, device, max_iter)
+        self.h = lib().armour_create(ctypes.byref(cfg))
+        if not self.h:
+            raise ArmourError(f"armour_create failed: {lib().armour_last_error().decode()}")
+        self.T = T
+        self.NJ = lib().armour_num_joints(self.h)
+        self.max_worlds = max_worlds
+        self._keep = []
+        self.O = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().armour_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def num_constraints(self, O):
+        return lib().armour_num_constraints(self.h, O)
+
+    def _worlds(self, worlds):
+        arr = (World * len(worlds))()
+        self._keep = []
+        for i, (q0, qd0, qdd0, qdes, obs) in enumerate(worlds):
+            w = arr[i]
+            for j in range(NF):
+                w.q0[j], w.qd0[j], w.qdd0[j], w.q_des[j] = q0[j], qd0[j], qdd0[j], qdes[j]
+            o = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, 12))
+            self._keep.append(o)
+            w.num_obstacles = o.shape[0]
+            w.obstacles = _ptr(o) if o.shape[0] else None
+        self.O = arr[0].num_obstacles
+        return arr
+
+    def plan(self, worlds):
+        arr = self._worlds(worlds)
+        res = (Result * len(worlds))()
+        tm = Timing()
+        _check(lib().armour_plan_batch(self.h, len(worlds), arr, res, ctypes.byref(tm)))
+        out = []
+        for r in res:
+            out.append(dict(k_opt=np.array(r.k_opt[:]), feasible=bool(r.feasible), status=r.solver_status,
+                            iterations=r.iterations, evaluations=r.evaluations, cost=r.cost, kkt=r.kkt_error))
+        return out, dict(reach_ms=tm.reach_ms, nlp_ms=tm.nlp_ms, total_ms=tm.total_ms)
+
+    def reach(self, worlds):
+        arr = self._worlds(worlds)
+        tm = Timing()
+        _check(lib().armour_reach_batch(self.h, len(worlds), arr, ctypes.byref(tm)))
+        return dict(reach_ms=tm.reach_ms, total_ms=tm.total_ms)
+
+    def eval_constraints(self, w, x, jac=True):
+        m = self.num_constraints(self.O)
+        x = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+        g = np.zeros(m)
+        J = np.zeros((m, NF)) if jac else None
+        _check(lib().armour_eval_constraints(self.h, w, _ptr(x), _ptr(g), _ptr(J)))
+        return (g, J) if jac else g
+
+    def constraints(self, w):
+        g = np.zeros(self.num_constraints(self.O))
+        _check(lib().armour_get_constraints(self.h, w, _ptr(g)))
+        return g
+
+    def link_centers(self, w):
+        c = np.zeros((self.T, self.NJ, 3))
+        _check(lib().armour_get_link_centers(self.h, w, _ptr(c)))
+        return c
+
+    def link_generators(self, w):
+        """[T, NJ, 3, 6] (the armour_joint_position_radius.out payload)"""
+        g = np.zeros((self.T, self.NJ, 3, 6))
+        _check(lib().armour_get_link_generators(self.h, w, _ptr(g)))
+        return g
+
+    def torque_radius(self, w):
+        r = np.zeros((self.T, NF))
+        _check(lib().armour_get_torque_radius(self.h, w, _ptr(r)))
+        return r
+
+
+__all__ = ["Planner", "ArmourError", "make_world", "example_world", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]

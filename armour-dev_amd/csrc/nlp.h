@@ -1,0 +1,75 @@
+// armour-mi355x — device data layout of the batched NLP (W worlds planned together).
+#pragma once
+#include "reach.h"
+
+namespace armour {
+
+constexpr int EVAL_THREADS = 256;
+constexpr int ROW_THREADS = 256;
+constexpr int MAX_FILTER = 64;
+constexpr int KA = 56;   // partial-sum slots per row block (pass A is the largest user)
+
+// solver options (oracle/src/ipm.h IpmOptions)
+struct IpmOpts {
+    double tol = 1e-4;
+    int max_iter = 100;
+    double mu0 = 0.1;
+    double kappa_eps = 10.0;
+    double kappa_mu = 0.2;
+    double theta_mu = 1.5;
+    double tau_min = 0.99;
+    double bound_push = 1e-2;
+    double eta = 1e-4;
+    int max_ls = 10;
+    double kappa_sigma = 1e10;
+    double s_max = 100.0;
+    double inf_bound = 1e19;
+};
+
+struct WorldState {
+    double x[NF], xt[NF], dx[NF];
+    double H[NF * NF];
+    double mu, alpha, ap, ad, theta0, phi0, Dphi, theta_max, theta_min, kkt;
+    double wa_old_a[NF], wa_old_b[NF];   // sum (z_lo - z_hi) a  and  sum (dz_lo - dz_hi) a at x
+    double filt_theta[MAX_FILTER], filt_phi[MAX_FILTER];
+    int nfilt;
+    int cur;           // eval slot holding the current point
+    int status;        // 0 running, 1 converged, 2 max_iter, 3 line-search failure
+    int searching;     // 1 while the line search of this iteration has not accepted
+    int accepted_ok;   // last acceptance passed the filter (0: forced after max_ls trials)
+    int ftype;
+    int first_update, nfail, iter, nevals, ls;
+};
+
+struct NlpDev {
+    int W, T, NJ, O, m, R, nblk, chunk;
+    const RobotParams* rp;
+    IpmOpts opt;
+    // per-world inputs
+    const double* q0;
+    const double* qd0;
+    const double* qdd0;
+    const double* qdes;
+    const double* obs;      // [W][O][12]
+    // reach outputs
+    ReachOut ro;
+    // hyperplanes [W][T][NJ][O][COMB], structure of arrays
+    double *hA0, *hA1, *hA2, *hd, *hdel;
+    // row bounds [W][R]
+    double *L, *U;
+    // evaluation slots: g [2][W][m], J [2][W][m][NF], f [2][W], grad [2][W][NF]
+    double* g;
+    double* J;
+    double* f;
+    double* grad;
+    double* link_c;         // [W][T][NJ][3] sliced link centres of the latest evaluation
+    // solver row state [W][R]
+    double *slo, *shi, *zlo, *zhi, *dslo, *dshi, *dzlo, *dzhi, *rplo, *rphi;
+    double* partial;        // [W][nblk][KA]
+    WorldState* ws;         // [W]
+    int* flags;             // [0]: any world still searching, [1]: any world running
+};
+
+AD long gidx(const NlpDev& d, int slot, int w, long r) { return ((long)slot * d.W + w) * d.m + r; }
+
+}  // namespace armour

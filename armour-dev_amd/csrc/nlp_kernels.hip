@@ -1,0 +1,827 @@
+// armour-mi355x — NLP kernels for a batch of W worlds:
+//   hyperplane_kernel   buffered-obstacle hyperplanes (KPR/CollisionChecking.cu:136-228)
+//   bounds_kernel       constraint bounds (KPR/NLPclass.cu:87-165)
+//   eval_kernel         g(x) and its dense Jacobian (KPR/NLPclass.cu:207-396): PZ slicing
+//                       (PZsparse.cu:404-555), collision rows (CollisionChecking.cu:230-299) with a
+//                       wave-wide argmax in the reference's scan order, torque and extremum rows
+//   ipm_*               armour-IPM (oracle/src/ipm.cpp), one row-parallel pass per phase with
+//                       deterministic block partials and one thread per world for the 7x7 algebra
+//   feasible_kernel     finalize_solution's re-check (KPR/NLPclass.cu:449-538)
+#include "nlp.h"
+
+namespace armour {
+
+// ------------------------------------------------------------------------------------------
+// helpers
+__device__ inline double ipow(double x, int d) { return d == 0 ? 1.0 : d == 1 ? x : d == 2 ? x * x : x * x * x; }
+
+__device__ inline double wave_sum(double v) {
+    for (int m = 32; m > 0; m >>= 1) v = v + __shfl_xor(v, m, 64);
+    return v;
+}
+__device__ inline double wave_max(double v) {
+    for (int m = 32; m > 0; m >>= 1) v = fmax(v, __shfl_xor(v, m, 64));
+    return v;
+}
+__device__ inline double wave_min(double v) {
+    for (int m = 32; m > 0; m >>= 1) v = fmin(v, __shfl_xor(v, m, 64));
+    return v;
+}
+// kind: 0 sum, 1 max, 2 min; result written by thread 0 to out
+__device__ inline void block_reduce(double v, int kind, double* lds, double* out) {
+    v = kind == 0 ? wave_sum(v) : kind == 1 ? wave_max(v) : wave_min(v);
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) lds[wave] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = lds[0];
+        for (int i = 1; i < nw; i++) s = kind == 0 ? s + lds[i] : kind == 1 ? fmax(s, lds[i]) : fmin(s, lds[i]);
+        *out = s;
+    }
+}
+
+__device__ inline bool has_lo(const NlpDev& d, double L) { return L > -d.opt.inf_bound; }
+__device__ inline bool has_hi(const NlpDev& d, double U) { return U < d.opt.inf_bound; }
+
+// value and gradient of row r of world w from eval slot `slot` at point x
+__device__ inline double row_va(const NlpDev& d, int slot, int w, int r, const double* x, double* a) {
+    if (r < d.m) {
+        const long gi = gidx(d, slot, w, r);
+        const double* J = d.J + gi * NF;
+#pragma unroll
+        for (int j = 0; j < NF; j++) a[j] = J[j];
+        return d.g[gi];
+    }
+#pragma unroll
+    for (int j = 0; j < NF; j++) a[j] = (j == r - d.m) ? 1.0 : 0.0;
+    return x[r - d.m];
+}
+
+// ------------------------------------------------------------------------------------------
+// hyperplanes: one thread per (world, t, link, obstacle, generator pair)
+__global__ void hyperplane_kernel(NlpDev d) {
+    const long total = (long)d.W * d.T * d.NJ * d.O * COMB;
+    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+        const int p = (int)(idx % COMB);
+        long rest = idx / COMB;
+        const int o = (int)(rest % d.O); rest /= d.O;
+        const int l = (int)(rest % d.NJ); rest /= d.NJ;
+        const int t = (int)(rest % d.T);
+        const int w = (int)(rest / d.T);
+        // pair table (CollisionChecking.cu:26-39): lexicographic pairs of the 9 buffered generators
+        int a = 0, rem = p;
+        while (rem >= BUF_GEN - 1 - a) { rem -= BUF_GEN - 1 - a; a++; }
+        const int b = a + 1 + rem;
+        const double* ob = d.obs + ((long)w * d.O + o) * 12;
+        const double* lg = d.ro.link_gens + (((long)w * d.T + t) * d.NJ + l) * 18;
+        double G[BUF_GEN][3];
+#pragma unroll
+        for (int i = 0; i < OBS_GEN; i++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[i][r] = ob[(i + 1) * 3 + r];
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[OBS_GEN + i][r] = lg[r + 3 * i];
+        double ga[3], gb[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            ga[r] = G[0][r]; gb[r] = G[1][r];
+        }
+        for (int i = 0; i < BUF_GEN; i++)
+            if (i == a) { ga[0] = G[i][0]; ga[1] = G[i][1]; ga[2] = G[i][2]; }
+        for (int i = 0; i < BUF_GEN; i++)
+            if (i == b) { gb[0] = G[i][0]; gb[1] = G[i][1]; gb[2] = G[i][2]; }
+        double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
+        double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
+        double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
+        const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
+        double C0 = 0, C1 = 0, C2 = 0;
+        if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
+        const double dd = C0 * ob[0] + C1 * ob[1] + C2 * ob[2];
+        double del = 0.0;
+#pragma unroll
+        for (int j = 0; j < BUF_GEN; j++) del += fabs(C0 * G[j][0] + C1 * G[j][1] + C2 * G[j][2]);
+        d.hA0[idx] = C0; d.hA1[idx] = C1; d.hA2[idx] = C2; d.hd[idx] = dd; d.hdel[idx] = del;
+    }
+}
+
+// constraint bounds (NLPclass.cu:87-165); rows m..m+NF-1 are the box bounds on x
+__global__ void bounds_kernel(NlpDev d) {
+    const RobotParams& rp = *d.rp;
+    const long total = (long)d.W * d.R;
+    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+        const int w = (int)(idx / d.R), r = (int)(idx % d.R);
+        double L, U;
+        const int nt = NF * d.T, nc = d.T * d.NJ * d.O;
+        if (r < nt) {
+            const int t = r / NF, j = r % NF;
+            const double tr = d.ro.torque_radius[((long)w * d.T + t) * NF + j];
+            L = -rp.torque_limits[j] + tr;
+            U = rp.torque_limits[j] - tr;
+        } else if (r < nt + nc) {
+            L = -1e19; U = 0;
+        } else if (r < nt + nc + 2 * NF) {
+            const int j = (r - nt - nc) % NF;
+            L = rp.state_lb[j] + rp.qe;
+            U = rp.state_ub[j] - rp.qe;
+        } else if (r < d.m) {
+            const int j = (r - nt - nc - 2 * NF) % NF;
+            L = -rp.speed_limits[j] + rp.qde;
+            U = rp.speed_limits[j] - rp.qde;
+        } else {
+            L = -1.0; U = 1.0;  // NLPclass.cu:105-113
+        }
+        d.L[idx] = L;
+        d.U[idx] = U;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// trajectory extrema (Trajectory.cu:256-540; restated as in oracle/src/traj.cpp)
+__device__ void extremum(int kind, double q0, double Tqd0, double TTqdd0, double ka, double* mn, double* mx, int* mnid, int* mxid, double* e2o, double* e3o) {
+    double e2, e3;
+    if (kind == 0) q_roots(Tqd0, TTqdd0, ka, &e2, &e3);
+    else qd_roots(Tqd0, TTqdd0, ka, &e2, &e3);
+    auto f = [&](double t) { return kind == 0 ? bz_q(q0, Tqd0, TTqdd0, ka, t) : bz_qd(q0, Tqd0, TTqdd0, ka, t); };
+    const double v1 = f(0.0), v2 = f(e2), v3 = f(e3), v4 = f(1.0);
+    if (v1 < v4) { *mn = v1; *mnid = 1; *mx = v4; *mxid = 4; }
+    else { *mn = v4; *mnid = 4; *mx = v1; *mxid = 1; }
+    if (0 <= e2 && e2 <= 1) {
+        if (v2 < *mn) { *mn = v2; *mnid = 2; }
+        if (*mx < v2) { *mx = v2; *mxid = 2; }
+    }
+    if (0 <= e3 && e3 <= 1) {
+        if (v3 < *mn) { *mn = v3; *mnid = 3; }
+        if (*mx < v3) { *mx = v3; *mxid = 3; }
+    }
+    *e2o = e2;
+    *e3o = e3;
+}
+__device__ double extremum_grad(int kind, int id, double e2, double e3) {
+    // envelope theorem: d/dk of the value at an interior critical point (oracle/src/traj.cpp)
+    if (id == 1) return 0.0;
+    if (id == 4) return 1.0;  // the reference returns 1 at t = 1 for both position and velocity
+    const double r = id == 2 ? e2 : e3;
+    return kind == 0 ? r * r * r * (6 * r * r - 15 * r + 10) : 30 * r * r * (r - 1) * (r - 1);
+}
+__device__ double wrap_to_pi(double a) {
+    double w = a;
+    while (w < -M_PI) w += 2 * M_PI;
+    while (w > M_PI) w -= 2 * M_PI;
+    return w;
+}
+
+// ------------------------------------------------------------------------------------------
+// g(x) and dense Jacobian. grid (T, W); mode 0: all worlds at ws.x into slot 0;
+// mode 1: searching worlds at ws.xt into slot 1 - cur
+__global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) {
+    const int t = blockIdx.x, w = blockIdx.y;
+    WorldState& S = d.ws[w];
+    if (mode == 1 && !(S.status == 0 && S.searching)) return;
+    const int slot = mode == 0 ? 0 : 1 - S.cur;
+    const RobotParams& rp = *d.rp;
+    __shared__ double x[NF];
+    __shared__ double lc[MAX_J][3];
+    __shared__ double dlc[MAX_J][NF][3];
+    if (threadIdx.x < NF) x[threadIdx.x] = mode == 0 ? S.x[threadIdx.x] : S.xt[threadIdx.x];
+    __syncthreads();
+    const long jt = (long)w * d.T + t;
+    // link slices: one thread per (link, component)  (PZsparse.cu:404-435, 477-516)
+    const int tid = threadIdx.x;
+    if (tid < d.NJ * 3) {
+        const int l = tid / 3, e = tid % 3;
+        const long base = jt * d.NJ + l;
+        const int cnt = d.ro.link_cnt[base];
+        double c = d.ro.link_center[base * 3 + e];
+        const double r = d.ro.link_rad[base * 3 + e];
+        double gr[NF];
+#pragma unroll
+        for (int k = 0; k < NF; k++) gr[k] = 0.0;
+        for (int q = 0; q < cnt; q++) {
+            const int h = d.ro.link_hash[base * CAP_LM + q];
+            const double co = d.ro.link_coef[(base * CAP_LM + q) * 3 + e];
+            int dg[NF];
+#pragma unroll
+            for (int j = 0; j < NF; j++) dg[j] = (h >> (2 * j)) & 3;
+            double v = co;
+#pragma unroll
+            for (int j = 0; j < NF; j++) if (dg[j]) v = v * ipow(x[j], dg[j]);
+            c = c + v;
+#pragma unroll
+            for (int k = 0; k < NF; k++) {
+                double tk = co;
+#pragma unroll
+                for (int j = 0; j < NF; j++) {
+                    if (j == k) tk = dg[j] == 0 ? 0.0 : tk * ((double)dg[j] * ipow(x[j], dg[j] - 1));
+                    else if (dg[j]) tk = tk * ipow(x[j], dg[j]);
+                }
+                gr[k] = gr[k] + tk;
+            }
+        }
+        const double cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
+        lc[l][e] = cc;
+        d.link_c[base * 3 + e] = cc;
+#pragma unroll
+        for (int k = 0; k < NF; k++) dlc[l][k][e] = gr[k];
+    } else if (tid >= 64 && tid < 64 + NF) {
+        // torque rows (NLPclass.cu:304-309, 376-380)
+        const int j = tid - 64;
+        const long base = jt * NF + j;
+        const int cnt = d.ro.tq_cnt[base];
+        double c = d.ro.tq_center[base];
+        const double r = d.ro.tq_rad[base];
+        double gr[NF];
+#pragma unroll
+        for (int k = 0; k < NF; k++) gr[k] = 0.0;
+        for (int q = 0; q < cnt; q++) {
+            const int h = d.ro.tq_hash[base * CAP_UM + q];
+            const double co = d.ro.tq_coef[base * CAP_UM + q];
+            int dg[NF];
+#pragma unroll
+            for (int jj = 0; jj < NF; jj++) dg[jj] = (h >> (2 * jj)) & 3;
+            double v = co;
+#pragma unroll
+            for (int jj = 0; jj < NF; jj++) if (dg[jj]) v = v * ipow(x[jj], dg[jj]);
+            c = c + v;
+#pragma unroll
+            for (int k = 0; k < NF; k++) {
+                double tk = co;
+#pragma unroll
+                for (int jj = 0; jj < NF; jj++) {
+                    if (jj == k) tk = dg[jj] == 0 ? 0.0 : tk * ((double)dg[jj] * ipow(x[jj], dg[jj] - 1));
+                    else if (dg[jj]) tk = tk * ipow(x[jj], dg[jj]);
+                }
+                gr[k] = gr[k] + tk;
+            }
+        }
+        const long row = (long)t * NF + j;
+        const long gi = gidx(d, slot, w, row);
+        d.g[gi] = ((c - r) + (c + r)) * 0.5;
+#pragma unroll
+        for (int k = 0; k < NF; k++) d.J[gi * NF + k] = gr[k];
+    } else if (tid == 128 && t == 0) {
+        // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267)
+        const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
+        const double* q0 = d.q0 + w * NF;
+        const double* qd0 = d.qd0 + w * NF;
+        const double* qdd0 = d.qdd0 + w * NF;
+        const double D = rp.duration;
+        for (int kind = 0; kind < 2; kind++)
+            for (int i = 0; i < NF; i++) {
+                const double Tq = qd0[i] * D, TTq = qdd0[i] * D * D;
+                const double ka = rp.k_range[i] * x[i];
+                double mn, mx, e2, e3;
+                int mnid, mxid;
+                extremum(kind, q0[i], Tq, TTq, ka, &mn, &mx, &mnid, &mxid, &e2, &e3);
+                const double scale = kind == 0 ? 1.0 : D;
+                const long rmin = off2 + kind * 2 * NF + i, rmax = rmin + NF;
+                const long gmin = gidx(d, slot, w, rmin), gmax = gidx(d, slot, w, rmax);
+                d.g[gmin] = mn / scale;
+                d.g[gmax] = mx / scale;
+                const double gmn = extremum_grad(kind, mnid, e2, e3) * rp.k_range[i] / scale;
+                const double gmx = extremum_grad(kind, mxid, e2, e3) * rp.k_range[i] / scale;
+#pragma unroll
+                for (int k = 0; k < NF; k++) {
+                    d.J[gmin * NF + k] = (k == i) ? gmn : 0.0;
+                    d.J[gmax * NF + k] = (k == i) ? gmx : 0.0;
+                }
+            }
+        // cost: wrapped joints summed first (NLPclass.cu:225-233)
+        const double tp = rp.t_plan;
+        double qp[NF];
+        for (int i = 0; i < NF; i++) qp[i] = bz_q(q0[i], qd0[i] * D, qdd0[i] * D * D, rp.k_range[i] * x[i], tp);
+        double fv = 0.0;
+        bool first = true;
+        for (int pass = 1; pass >= 0; pass--)
+            for (int i = 0; i < NF; i++) {
+                if (rp.wrap_mask[i] != pass) continue;
+                const double dd = pass ? wrap_to_pi(d.qdes[w * NF + i] - qp[i]) : (d.qdes[w * NF + i] - qp[i]);
+                const double term = dd * dd;
+                fv = first ? term : fv + term;
+                first = false;
+            }
+        d.f[slot * d.W + w] = fv * rp.cost_scale;
+        for (int i = 0; i < NF; i++) {
+            const double dk = tp * tp * tp * (6 * tp * tp - 15 * tp + 10) * rp.k_range[i];
+            double gv = rp.wrap_mask[i] ? (2 * wrap_to_pi(qp[i] - d.qdes[w * NF + i]) * dk) : (2 * (qp[i] - d.qdes[w * NF + i]) * dk);
+            d.grad[((long)slot * d.W + w) * NF + i] = gv * rp.cost_scale;
+        }
+    }
+    __syncthreads();
+    // collision rows: one wavefront per (link, obstacle); lane p evaluates hyperplane p and the
+    // wave takes the first maximum in the reference's scan order (pos_0, neg_0, pos_1, ...)
+    const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const long nt = (long)NF * d.T;
+    for (int pr = wave; pr < d.NJ * d.O; pr += nw) {
+        const int l = pr / d.O, o = pr % d.O;
+        const long pb = ((jt * d.NJ + l) * d.O + o) * COMB;
+        double best = -100000000.0;
+        int seq = 1 << 30;
+        double A0 = 0, A1 = 0, A2 = 0;
+        if (lane < COMB) {
+            A0 = d.hA0[pb + lane]; A1 = d.hA1[pb + lane]; A2 = d.hA2[pb + lane];
+            const double dd = d.hd[pb + lane], del = d.hdel[pb + lane];
+            const double nrm = sqrt(A0 * A0 + A1 * A1 + A2 * A2);
+            if (nrm > 0) {
+                const double Ac = A0 * lc[l][0] + A1 * lc[l][1] + A2 * lc[l][2];
+                const double pos = Ac - (dd + del);
+                const double neg = -Ac - (-dd + del);
+                if (pos > best) { best = pos; seq = 2 * lane; }
+                if (neg > best) { best = neg; seq = 2 * lane + 1; }
+            }
+        }
+        for (int m = 32; m > 0; m >>= 1) {
+            const double ob = __shfl_xor(best, m, 64);
+            const int os = __shfl_xor(seq, m, 64);
+            if (ob > best || (ob == best && os < seq)) { best = ob; seq = os; }
+        }
+        const int id = seq < (1 << 30) ? (seq >> 1) : 0;
+        const bool isneg = seq < (1 << 30) && (seq & 1);
+        const double B0 = __shfl(A0, id, 64), B1 = __shfl(A1, id, 64), B2 = __shfl(A2, id, 64);
+        const long row = nt + ((long)l * d.T + t) * d.O + o;
+        const long gi = gidx(d, slot, w, row);
+        if (lane == 0) d.g[gi] = -best;
+        if (lane < NF) {
+            const double dot = B0 * dlc[l][lane][0] + B1 * dlc[l][lane][1] + B2 * dlc[l][lane][2];
+            d.J[gi * NF + lane] = isneg ? dot : -dot;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// armour-IPM
+__global__ void ipm_world_init(NlpDev d) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= d.W) return;
+    WorldState& S = d.ws[w];
+    for (int j = 0; j < NF; j++) {
+        const double xl = -1.0, xu = 1.0;
+        const double p = fmin(d.opt.bound_push * fmax(1.0, fabs(xl)), d.opt.bound_push * (xu - xl));
+        S.x[j] = fmin(fmax(0.0, xl + p), xu - p);  // start point x = 0 (NLPclass.cu:193-199)
+        S.xt[j] = S.x[j];
+        S.dx[j] = 0.0;
+    }
+    for (int i = 0; i < NF * NF; i++) S.H[i] = (i % (NF + 1) == 0) ? 1.0 : 0.0;
+    S.mu = d.opt.mu0;
+    S.theta_max = -1;
+    S.theta_min = -1;
+    S.nfilt = 0;
+    S.cur = 0;
+    S.status = 0;
+    S.searching = 0;
+    S.first_update = 1;
+    S.nfail = 0;
+    S.iter = 0;
+    S.nevals = 1;
+    S.kkt = 0;
+}
+
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
+    const int w = blockIdx.y;
+    const WorldState& S = d.ws[w];
+    const long r0 = (long)blockIdx.x * d.chunk;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        double a[NF];
+        const double v = row_va(d, S.cur, w, (int)r, S.x, a);
+        const long i = (long)w * d.R + r;
+        const double L = d.L[i], U = d.U[i];
+        const bool hl = has_lo(d, L), hh = has_hi(d, U);
+        double p = 0;
+        if (hl && hh) p = fmin(d.opt.bound_push * fmax(1.0, fabs(L)), d.opt.bound_push * (U - L));
+        d.slo[i] = 0; d.zlo[i] = 0; d.shi[i] = 0; d.zhi[i] = 0;
+        if (hl) {
+            const double pl = hh ? p : d.opt.bound_push * fmax(1.0, fabs(L));
+            d.slo[i] = fmax(v - L, pl);
+            d.zlo[i] = S.mu / d.slo[i];
+        }
+        if (hh) {
+            const double pu = hl ? p : d.opt.bound_push * fmax(1.0, fabs(U));
+            d.shi[i] = fmax(U - v, pu);
+            d.zhi[i] = S.mu / d.shi[i];
+        }
+    }
+}
+
+// pass A: residuals, errors, reduced Newton system sums
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
+    const int w = blockIdx.y;
+    const WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    __shared__ double lds[ROW_THREADS / 64];
+    double rdp[NF], M[28], u1[NF], u2[NF];
+    double inf_p = 0, compl0 = 0, cm = 0, sumz = 0;
+#pragma unroll
+    for (int j = 0; j < NF; j++) { rdp[j] = 0; u1[j] = 0; u2[j] = 0; }
+#pragma unroll
+    for (int k = 0; k < 28; k++) M[k] = 0;
+    const double mu = S.mu;
+    const long r0 = (long)blockIdx.x * d.chunk;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        double a[NF];
+        const double v = row_va(d, S.cur, w, (int)r, S.x, a);
+        const long i = (long)w * d.R + r;
+        const double L = d.L[i], U = d.U[i];
+        double wr = 0, sig = 0, c1 = 0, c2 = 0;
+        if (has_lo(d, L)) {
+            const double s = d.slo[i], z = d.zlo[i];
+            const double rp = (v - L) - s;
+            d.rplo[i] = rp;
+            wr += z;
+            inf_p = fmax(inf_p, fabs(rp));
+            compl0 = fmax(compl0, s * z);
+            cm = fmax(cm, fabs(s * z - mu));
+            sumz += z;
+            const double sg = z / s;
+            sig += sg;
+            c1 += 1.0 / s;
+            c2 += sg * rp;
+        }
+        if (has_hi(d, U)) {
+            const double s = d.shi[i], z = d.zhi[i];
+            const double rp = (U - v) - s;
+            d.rphi[i] = rp;
+            wr -= z;
+            inf_p = fmax(inf_p, fabs(rp));
+            compl0 = fmax(compl0, s * z);
+            cm = fmax(cm, fabs(s * z - mu));
+            sumz += z;
+            const double sg = z / s;
+            sig += sg;
+            c1 -= 1.0 / s;
+            c2 -= sg * rp;
+        }
+        int k = 0;
+#pragma unroll
+        for (int p = 0; p < NF; p++) {
+            rdp[p] += wr * a[p];
+            u1[p] += a[p] * c1;
+            u2[p] += a[p] * c2;
+#pragma unroll
+            for (int q = p; q < NF; q++) M[k++] += sig * a[p] * a[q];
+        }
+    }
+    double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
+#pragma unroll
+    for (int j = 0; j < NF; j++) block_reduce(rdp[j], 0, lds, &out[j]);
+    block_reduce(inf_p, 1, lds, &out[7]);
+    block_reduce(compl0, 1, lds, &out[8]);
+    block_reduce(cm, 1, lds, &out[9]);
+    block_reduce(sumz, 0, lds, &out[10]);
+#pragma unroll
+    for (int k = 0; k < 28; k++) block_reduce(M[k], 0, lds, &out[11 + k]);
+#pragma unroll
+    for (int j = 0; j < NF; j++) block_reduce(u1[j], 0, lds, &out[39 + j]);
+#pragma unroll
+    for (int j = 0; j < NF; j++) block_reduce(u2[j], 0, lds, &out[46 + j]);
+}
+
+__device__ bool chol_solve7(const double* M, double shift, const double* b, double* x) {
+    double L[NF * NF];
+    for (int i = 0; i < NF; i++)
+        for (int j = 0; j <= i; j++) {
+            double s = M[i * NF + j] + (i == j ? shift : 0.0);
+            for (int k = 0; k < j; k++) s -= L[i * NF + k] * L[j * NF + k];
+            if (i == j) {
+                if (!(s > 0)) return false;
+                L[i * NF + i] = sqrt(s);
+            } else {
+                L[i * NF + j] = s / L[j * NF + j];
+            }
+        }
+    double y[NF];
+    for (int i = 0; i < NF; i++) {
+        double s = b[i];
+        for (int k = 0; k < i; k++) s -= L[i * NF + k] * y[k];
+        y[i] = s / L[i * NF + i];
+    }
+    for (int i = NF - 1; i >= 0; i--) {
+        double s = y[i];
+        for (int k = i + 1; k < NF; k++) s -= L[k * NF + i] * x[k];
+        x[i] = s / L[i * NF + i];
+    }
+    return true;
+}
+
+__global__ void ipm_world_A(NlpDev d, int nside) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= d.W) return;
+    WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    if (S.iter >= d.opt.max_iter) { S.status = 2; return; }  // oracle: loop ends without a final check
+    double P[KA];
+    for (int k = 0; k < 53; k++) P[k] = 0;
+    for (int b = 0; b < d.nblk; b++) {
+        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
+        for (int k = 0; k < 53; k++) {
+            if (k >= 7 && k <= 9) P[k] = fmax(P[k], in[k]);
+            else P[k] = P[k] + in[k];
+        }
+    }
+    const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
+    double rd[NF], inf_d = 0;
+    for (int j = 0; j < NF; j++) { rd[j] = grad[j] - P[j]; inf_d = fmax(inf_d, fabs(rd[j])); }
+    const double sd = fmax(d.opt.s_max, P[10] / (double)(nside > 0 ? nside : 1)) / d.opt.s_max;
+    const double E0 = fmax(fmax(inf_d / sd, P[7]), P[8] / sd);
+    S.kkt = E0;
+    if (E0 <= d.opt.tol) { S.status = 1; return; }
+    const double Emu = fmax(fmax(inf_d / sd, P[7]), P[9] / sd);
+    if (Emu <= d.opt.kappa_eps * S.mu && S.mu > d.opt.tol / 10) {
+        S.mu = fmax(d.opt.tol / 10, fmin(d.opt.kappa_mu * S.mu, pow(S.mu, d.opt.theta_mu)));
+        S.nfilt = 0;
+    }
+    double M[NF * NF], rhs[NF];
+    int k = 0;
+    for (int p = 0; p < NF; p++)
+        for (int q = p; q < NF; q++) {
+            M[p * NF + q] = S.H[p * NF + q] + P[11 + k];
+            M[q * NF + p] = S.H[q * NF + p] + P[11 + k];
+            k++;
+        }
+    for (int j = 0; j < NF; j++) rhs[j] = -grad[j] + S.mu * P[39 + j] - P[46 + j];
+    // inertia correction: shift the diagonal until the factorisation succeeds (bounded)
+    double shift = 0.0;
+    bool ok = false;
+    for (int tries = 0; tries < 40 && !ok; tries++) {
+        ok = chol_solve7(M, shift, rhs, S.dx);
+        shift = (shift == 0.0) ? 1e-8 : shift * 10;
+    }
+    if (!ok) {
+        for (int j = 0; j < NF; j++) S.dx[j] = 0.0;
+        S.status = 3;
+    }
+}
+
+// pass B: step components, fraction to boundary, line-search ingredients
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
+    const int w = blockIdx.y;
+    const WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    __shared__ double lds[ROW_THREADS / 64];
+    const double mu = S.mu;
+    const double tau = fmax(d.opt.tau_min, 1.0 - mu);
+    double ap = 1.0, ad = 1.0, rp1 = 0, bdir = 0, logs = 0, wa[NF], wb[NF];
+#pragma unroll
+    for (int j = 0; j < NF; j++) { wa[j] = 0; wb[j] = 0; }
+    const long r0 = (long)blockIdx.x * d.chunk;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        double a[NF];
+        row_va(d, S.cur, w, (int)r, S.x, a);
+        double adx = 0;
+#pragma unroll
+        for (int j = 0; j < NF; j++) adx += a[j] * S.dx[j];
+        const long i = (long)w * d.R + r;
+        const double L = d.L[i], U = d.U[i];
+        double za = 0, zb = 0;
+        if (has_lo(d, L)) {
+            const double s = d.slo[i], z = d.zlo[i], sg = z / s;
+            const double ds = adx + d.rplo[i];
+            const double dz = mu / s - z - sg * ds;
+            d.dslo[i] = ds; d.dzlo[i] = dz;
+            if (ds < 0) ap = fmin(ap, -tau * s / ds);
+            if (dz < 0) ad = fmin(ad, -tau * z / dz);
+            rp1 += fabs(d.rplo[i]); bdir += ds / s; logs += log(s);
+            za += z; zb += dz;
+        }
+        if (has_hi(d, U)) {
+            const double s = d.shi[i], z = d.zhi[i], sg = z / s;
+            const double ds = -adx + d.rphi[i];
+            const double dz = mu / s - z - sg * ds;
+            d.dshi[i] = ds; d.dzhi[i] = dz;
+            if (ds < 0) ap = fmin(ap, -tau * s / ds);
+            if (dz < 0) ad = fmin(ad, -tau * z / dz);
+            rp1 += fabs(d.rphi[i]); bdir += ds / s; logs += log(s);
+            za -= z; zb -= dz;
+        }
+#pragma unroll
+        for (int j = 0; j < NF; j++) { wa[j] += za * a[j]; wb[j] += zb * a[j]; }
+    }
+    double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
+    block_reduce(ap, 2, lds, &out[0]);
+    block_reduce(ad, 2, lds, &out[1]);
+    block_reduce(rp1, 0, lds, &out[2]);
+    block_reduce(bdir, 0, lds, &out[3]);
+    block_reduce(logs, 0, lds, &out[4]);
+#pragma unroll
+    for (int j = 0; j < NF; j++) block_reduce(wa[j], 0, lds, &out[5 + j]);
+#pragma unroll
+    for (int j = 0; j < NF; j++) block_reduce(wb[j], 0, lds, &out[12 + j]);
+}
+
+__global__ void ipm_world_B(NlpDev d) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= d.W) return;
+    WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    double P[19];
+    P[0] = 1.0; P[1] = 1.0;
+    for (int k = 2; k < 19; k++) P[k] = 0;
+    for (int b = 0; b < d.nblk; b++) {
+        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
+        P[0] = fmin(P[0], in[0]);
+        P[1] = fmin(P[1], in[1]);
+        for (int k = 2; k < 19; k++) P[k] = P[k] + in[k];
+    }
+    const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
+    const double f = d.f[S.cur * d.W + w];
+    double gdx = 0;
+    for (int j = 0; j < NF; j++) gdx += grad[j] * S.dx[j];
+    S.ap = P[0];
+    S.ad = P[1];
+    S.theta0 = P[2];
+    if (S.theta_min < 0) S.theta_min = 1e-4 * fmax(1.0, S.theta0);
+    if (S.theta_max < 0) S.theta_max = 1e4 * fmax(1.0, S.theta0);
+    S.phi0 = f - S.mu * P[4];
+    S.Dphi = gdx - S.mu * P[3];
+    for (int j = 0; j < NF; j++) { S.wa_old_a[j] = P[5 + j]; S.wa_old_b[j] = P[12 + j]; }
+    S.alpha = S.ap;
+    for (int j = 0; j < NF; j++) S.xt[j] = S.x[j] + S.alpha * S.dx[j];
+    S.searching = 1;
+    S.ls = 0;
+    S.ftype = 0;
+    S.accepted_ok = 0;
+}
+
+// pass C: barrier objective and constraint violation at the trial point
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
+    const int w = blockIdx.y;
+    const WorldState& S = d.ws[w];
+    if (!(S.status == 0 && S.searching)) return;
+    __shared__ double lds[ROW_THREADS / 64];
+    double logt = 0, rpt = 0;
+    const long r0 = (long)blockIdx.x * d.chunk;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        double a[NF];
+        const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
+        const long i = (long)w * d.R + r;
+        const double L = d.L[i], U = d.U[i];
+        if (has_lo(d, L)) { const double st = d.slo[i] + S.alpha * d.dslo[i]; logt += log(st); rpt += fabs((v - L) - st); }
+        if (has_hi(d, U)) { const double st = d.shi[i] + S.alpha * d.dshi[i]; logt += log(st); rpt += fabs((U - v) - st); }
+    }
+    double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
+    block_reduce(logt, 0, lds, &out[0]);
+    block_reduce(rpt, 0, lds, &out[1]);
+}
+
+__global__ void ipm_world_C(NlpDev d) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= d.W) return;
+    WorldState& S = d.ws[w];
+    if (!(S.status == 0 && S.searching)) return;
+    double logt = 0, rpt = 0;
+    for (int b = 0; b < d.nblk; b++) {
+        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
+        logt = logt + in[0];
+        rpt = rpt + in[1];
+    }
+    S.nevals++;
+    const double ft = d.f[(1 - S.cur) * d.W + w];
+    const double phit = ft - S.mu * logt, thetat = rpt;
+    bool ok = thetat <= S.theta_max;
+    for (int q = 0; ok && q < S.nfilt; q++)
+        if (!(thetat < S.filt_theta[q] || phit < S.filt_phi[q])) ok = false;
+    bool ftype = false;
+    if (ok) {
+        const bool switching = S.Dphi < 0 && S.alpha * pow(-S.Dphi, 2.3) > pow(S.theta0, 1.1);
+        if (switching && S.theta0 <= S.theta_min) {
+            ok = phit <= S.phi0 + d.opt.eta * S.alpha * S.Dphi;
+            ftype = ok;
+        } else {
+            ok = thetat <= (1 - 1e-5) * S.theta0 || phit <= S.phi0 - 1e-8 * S.theta0;
+            if (!ok && switching) { ok = phit <= S.phi0 + d.opt.eta * S.alpha * S.Dphi; ftype = ok; }
+        }
+    }
+    if (ok) {
+        S.searching = 0;
+        S.accepted_ok = 1;
+        if (!ftype && S.nfilt < MAX_FILTER) {
+            S.filt_theta[S.nfilt] = (1 - 1e-5) * S.theta0;
+            S.filt_phi[S.nfilt] = S.phi0 - 1e-8 * S.theta0;
+            S.nfilt++;
+        }
+        return;
+    }
+    S.ls++;
+    if (S.ls >= d.opt.max_ls) {  // keep the last trial (oracle: accepted = false)
+        S.searching = 0;
+        S.accepted_ok = 0;
+        return;
+    }
+    S.alpha *= 0.5;
+    for (int j = 0; j < NF; j++) S.xt[j] = S.x[j] + S.alpha * S.dx[j];
+    atomicOr(&d.flags[0], 1);
+}
+
+// pass D: accept the trial point — slacks, multipliers, BFGS ingredients
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
+    const int w = blockIdx.y;
+    const WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    __shared__ double lds[ROW_THREADS / 64];
+    const double mu = S.mu, ad = S.ad, alpha = S.alpha, ks = d.opt.kappa_sigma;
+    double wn[NF];
+#pragma unroll
+    for (int j = 0; j < NF; j++) wn[j] = 0;
+    const long r0 = (long)blockIdx.x * d.chunk;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        double a[NF];
+        row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
+        const long i = (long)w * d.R + r;
+        const double L = d.L[i], U = d.U[i];
+        double wv = 0;
+        if (has_lo(d, L)) {
+            const double zn = d.zlo[i] + ad * d.dzlo[i];
+            wv += zn;
+            const double s = d.slo[i] + alpha * d.dslo[i];
+            d.slo[i] = s;
+            d.zlo[i] = fmin(fmax(zn, mu / (ks * s)), ks * mu / s);
+        }
+        if (has_hi(d, U)) {
+            const double zn = d.zhi[i] + ad * d.dzhi[i];
+            wv -= zn;
+            const double s = d.shi[i] + alpha * d.dshi[i];
+            d.shi[i] = s;
+            d.zhi[i] = fmin(fmax(zn, mu / (ks * s)), ks * mu / s);
+        }
+#pragma unroll
+        for (int j = 0; j < NF; j++) wn[j] += wv * a[j];
+    }
+    double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
+#pragma unroll
+    for (int j = 0; j < NF; j++) block_reduce(wn[j], 0, lds, &out[j]);
+}
+
+__global__ void ipm_world_D(NlpDev d) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= d.W) return;
+    WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    double wn[NF];
+    for (int j = 0; j < NF; j++) wn[j] = 0;
+    for (int b = 0; b < d.nblk; b++) {
+        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
+        for (int j = 0; j < NF; j++) wn[j] = wn[j] + in[j];
+    }
+    const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
+    const double* gradt = d.grad + ((long)(1 - S.cur) * d.W + w) * NF;
+    double sv[NF], y[NF], Hs[NF], ss = 0, sy = 0;
+    for (int j = 0; j < NF; j++) {
+        sv[j] = S.xt[j] - S.x[j];
+        const double wo = S.wa_old_a[j] + S.ad * S.wa_old_b[j];
+        y[j] = (gradt[j] - grad[j]) - (wn[j] - wo);
+        ss += sv[j] * sv[j];
+    }
+    for (int j = 0; j < NF; j++) sy += sv[j] * y[j];
+    if (S.first_update && sy > 0 && ss > 1e-20) {
+        double yy = 0;
+        for (int j = 0; j < NF; j++) yy += y[j] * y[j];
+        const double sc = yy / sy;
+        for (int i = 0; i < NF * NF; i++) S.H[i] = (i % (NF + 1) == 0) ? sc : 0.0;
+        S.first_update = 0;
+    }
+    double sHs = 0;
+    for (int i = 0; i < NF; i++) {
+        Hs[i] = 0;
+        for (int j = 0; j < NF; j++) Hs[i] += S.H[i * NF + j] * sv[j];
+        sHs += sv[i] * Hs[i];
+    }
+    if (ss > 1e-20 && sHs > 1e-20) {
+        const double theta = (sy >= 0.2 * sHs) ? 1.0 : 0.8 * sHs / (sHs - sy);
+        double rv[NF], sr = 0;
+        for (int j = 0; j < NF; j++) { rv[j] = theta * y[j] + (1 - theta) * Hs[j]; sr += sv[j] * rv[j]; }
+        if (sr > 1e-20)
+            for (int i = 0; i < NF; i++)
+                for (int j = 0; j < NF; j++) S.H[i * NF + j] += -Hs[i] * Hs[j] / sHs + rv[i] * rv[j] / sr;
+    }
+    for (int j = 0; j < NF; j++) S.x[j] = S.xt[j];
+    S.cur = 1 - S.cur;
+    S.nfail = S.accepted_ok ? 0 : S.nfail + 1;
+    S.iter++;
+    if (S.nfail >= 3) S.status = 3;
+    if (S.status == 0) atomicOr(&d.flags[1], 1);
+}
+
+// finalize_solution's feasibility re-check (NLPclass.cu:449-538): one block per world
+__global__ void feasible_kernel(NlpDev d, int* feasible) {
+    const int w = blockIdx.x;
+    const WorldState& S = d.ws[w];
+    const RobotParams& rp = *d.rp;
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const int nt = NF * d.T, nc = d.T * d.NJ * d.O;
+    for (int r = threadIdx.x; r < d.m; r += blockDim.x) {
+        const double v = d.g[gidx(d, S.cur, w, r)];
+        const long i = (long)w * d.R + r;
+        bool b;
+        if (r < nt) b = v < d.L[i] - rp.torque_violation || v > d.U[i] + rp.torque_violation;
+        else if (r < nt + nc) b = v > rp.collision_violation;
+        else b = v < d.L[i] || v > d.U[i];
+        if (b) atomicOr(&bad, 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) feasible[w] = bad ? 0 : 1;
+}
+
+}  // namespace armour

@@ -1,0 +1,428 @@
+// armour-mi355x — host runtime and C ABI (include/armour_hip.h).
+//
+// One planner handle owns a HIP stream and every device buffer for up to max_worlds worlds of
+// T time steps and max_obstacles obstacles, allocated once (the reference allocates per process,
+// KPR/CollisionChecking.cu:17-53). A batch runs entirely on the device:
+//   reach_kernel (JRS + PZ FK/RNEA + torque radius) -> hyperplane_kernel -> bounds_kernel ->
+//   armour-IPM passes (eval_kernel + ipm_rows_* / ipm_world_*) -> feasible_kernel;
+// the host only sequences launches and reads one flag word per line-search round.
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/armour_hip.h"
+#include "nlp_kernels.hip"
+#include "reach_kernel.hip"
+#include "robots.h"
+
+using namespace armour;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCK(expr)                                                                               \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return fail(ARMOUR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+    return hipMalloc((void**)p, sizeof(T) * (n > 0 ? n : 1));
+}
+}  // namespace
+
+struct armour_planner {
+    armour_config cfg;
+    int T = 0, NJ = 0, Omax = 0, Wmax = 0, ncu = 0, reach_grid = 0;
+    RobotParams rp;
+    RobotParams* d_rp = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4];
+    // inputs
+    double *q0 = nullptr, *qd0 = nullptr, *qdd0 = nullptr, *qdes = nullptr, *obs = nullptr, *xin = nullptr;
+    // reach
+    ReachOut ro;
+    ReachArgs ra;
+    // nlp
+    NlpDev d;
+    int* feas = nullptr;
+    int* flags = nullptr;     // device
+    int* h_flags = nullptr;   // pinned host
+    WorldState* h_ws = nullptr;
+    double* h_f = nullptr;
+    int* h_feas = nullptr;
+    // state of the last batch
+    int W = 0, O = 0;
+    bool reached = false, planned = false;
+    std::vector<void*> allocs;
+
+    template <class T>
+    int alloc(T** p, size_t n) {
+        hipError_t e = dalloc(p, n);
+        if (e != hipSuccess) return fail(ARMOUR_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+        allocs.push_back((void*)*p);
+        return 0;
+    }
+};
+
+static int planner_init(armour_planner* p, const armour_config* cfg) {
+    p->cfg = *cfg;
+    if (cfg->robot != 0) return fail(ARMOUR_E_ARG, "unknown robot id");
+    if (cfg->num_time_steps <= 0 || (cfg->num_time_steps % 2) != 0)
+        return fail(ARMOUR_E_ARG, "num_time_steps must be a positive even number (KPR/Parameters.h:16)");
+    if (cfg->max_obstacles < 0 || cfg->max_worlds <= 0) return fail(ARMOUR_E_ARG, "bad max_obstacles / max_worlds");
+    if (cfg->device >= 0) HIPCK(hipSetDevice(cfg->device));
+    int dev = 0;
+    HIPCK(hipGetDevice(&dev));
+    HIPCK(hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    kinova_gen3(p->rp);
+    p->T = cfg->num_time_steps;
+    p->NJ = p->rp.num_joints;
+    p->Omax = cfg->max_obstacles;
+    p->Wmax = cfg->max_worlds;
+    HIPCK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    for (int i = 0; i < 4; i++) HIPCK(hipEventCreate(&p->ev[i]));
+    const int T = p->T, NJ = p->NJ, Om = p->Omax > 0 ? p->Omax : 1, Wm = p->Wmax;
+    int rc = 0;
+    if ((rc = p->alloc(&p->d_rp, 1))) return rc;
+    HIPCK(hipMemcpy(p->d_rp, &p->rp, sizeof(RobotParams), hipMemcpyHostToDevice));
+    if ((rc = p->alloc(&p->q0, (size_t)Wm * NF)) || (rc = p->alloc(&p->qd0, (size_t)Wm * NF)) ||
+        (rc = p->alloc(&p->qdd0, (size_t)Wm * NF)) || (rc = p->alloc(&p->qdes, (size_t)Wm * NF)) ||
+        (rc = p->alloc(&p->xin, (size_t)Wm * NF)) || (rc = p->alloc(&p->obs, (size_t)Wm * Om * 12)))
+        return rc;
+    // reach outputs
+    const size_t jobs = (size_t)Wm * T;
+    ReachOut& ro = p->ro;
+    ro.T = T;
+    ro.NJ = NJ;
+    if ((rc = p->alloc(&ro.link_hash, jobs * NJ * CAP_LM)) || (rc = p->alloc(&ro.link_coef, jobs * NJ * CAP_LM * 3)) ||
+        (rc = p->alloc(&ro.link_cnt, jobs * NJ)) || (rc = p->alloc(&ro.link_center, jobs * NJ * 3)) ||
+        (rc = p->alloc(&ro.link_rad, jobs * NJ * 3)) || (rc = p->alloc(&ro.link_gens, jobs * NJ * 18)) ||
+        (rc = p->alloc(&ro.tq_hash, jobs * NF * CAP_UM)) || (rc = p->alloc(&ro.tq_coef, jobs * NF * CAP_UM)) ||
+        (rc = p->alloc(&ro.tq_cnt, jobs * NF)) || (rc = p->alloc(&ro.tq_center, jobs * NF)) ||
+        (rc = p->alloc(&ro.tq_rad, jobs * NF)) || (rc = p->alloc(&ro.torque_radius, jobs * NF)) ||
+        (rc = p->alloc(&ro.err, (size_t)Wm)))
+        return rc;
+    // reach workspace: two resident workgroups per CU, each with a private arena
+    p->reach_grid = 2 * p->ncu;
+    ReachArgs& ra = p->ra;
+    ra.arena_cap = 1 << 17;
+    ra.gcap = 1 << 15;
+    if ((rc = p->alloc(&ra.arena_h, (size_t)p->reach_grid * ra.arena_cap)) ||
+        (rc = p->alloc(&ra.arena_c, (size_t)p->reach_grid * ra.arena_cap * 3)) ||
+        (rc = p->alloc(&ra.gkh, (size_t)p->reach_grid * ra.gcap)) || (rc = p->alloc(&ra.gki, (size_t)p->reach_grid * ra.gcap)) ||
+        (rc = p->alloc(&ra.gkp, (size_t)p->reach_grid * ra.gcap)))
+        return rc;
+    // NLP
+    NlpDev& d = p->d;
+    d.rp = p->d_rp;
+    d.T = T;
+    d.NJ = NJ;
+    d.ro = ro;
+    if (cfg->max_iter > 0) d.opt.max_iter = cfg->max_iter;
+    const size_t mmax = (size_t)NF * T + (size_t)T * NJ * Om + NF * 4;
+    const size_t Rmax = mmax + NF;
+    const size_t planes = (size_t)Wm * T * NJ * Om * COMB;
+    if ((rc = p->alloc(&d.hA0, planes)) || (rc = p->alloc(&d.hA1, planes)) || (rc = p->alloc(&d.hA2, planes)) ||
+        (rc = p->alloc(&d.hd, planes)) || (rc = p->alloc(&d.hdel, planes)))
+        return rc;
+    if ((rc = p->alloc(&d.L, Wm * Rmax)) || (rc = p->alloc(&d.U, Wm * Rmax)) || (rc = p->alloc(&d.g, 2 * Wm * mmax)) ||
+        (rc = p->alloc(&d.J, 2 * Wm * mmax * NF)) || (rc = p->alloc(&d.f, 2 * (size_t)Wm)) ||
+        (rc = p->alloc(&d.grad, 2 * (size_t)Wm * NF)) || (rc = p->alloc(&d.link_c, jobs * NJ * 3)))
+        return rc;
+    double** rowbufs[] = {&d.slo, &d.shi, &d.zlo, &d.zhi, &d.dslo, &d.dshi, &d.dzlo, &d.dzhi, &d.rplo, &d.rphi};
+    for (double** b : rowbufs)
+        if ((rc = p->alloc(b, Wm * Rmax))) return rc;
+    const int nblk_max = (int)((Rmax + 2047) / 2048);
+    if ((rc = p->alloc(&d.partial, (size_t)Wm * nblk_max * KA)) || (rc = p->alloc(&d.ws, (size_t)Wm)) ||
+        (rc = p->alloc(&d.flags, 4)) || (rc = p->alloc(&p->feas, (size_t)Wm)))
+        return rc;
+    HIPCK(hipHostMalloc((void**)&p->h_flags, 4 * sizeof(int)));
+    HIPCK(hipHostMalloc((void**)&p->h_ws, Wm * sizeof(WorldState)));
+    HIPCK(hipHostMalloc((void**)&p->h_f, 2 * Wm * sizeof(double)));
+    HIPCK(hipHostMalloc((void**)&p->h_feas, Wm * sizeof(int)));
+    d.q0 = p->q0;
+    d.qd0 = p->qd0;
+    d.qdd0 = p->qdd0;
+    d.qdes = p->qdes;
+    d.obs = p->obs;
+    return 0;
+}
+
+static int upload_worlds(armour_planner* p, int W, const armour_world* worlds) {
+    if (W <= 0 || W > p->Wmax || !worlds) return fail(ARMOUR_E_ARG, "num_worlds out of range");
+    const int O = worlds[0].num_obstacles;
+    if (O < 0 || O > p->Omax) return fail(ARMOUR_E_ARG, "num_obstacles exceeds max_obstacles");
+    std::vector<double> a(4 * (size_t)W * NF), ob((size_t)W * (O > 0 ? O : 1) * 12, 0.0);
+    for (int w = 0; w < W; w++) {
+        if (worlds[w].num_obstacles != O) return fail(ARMOUR_E_ARG, "all worlds of a batch must have the same num_obstacles");
+        if (O > 0 && !worlds[w].obstacles) return fail(ARMOUR_E_ARG, "null obstacles");
+        for (int i = 0; i < NF; i++) {
+            a[0 * (size_t)W * NF + w * NF + i] = worlds[w].q0[i];
+            a[1 * (size_t)W * NF + w * NF + i] = worlds[w].qd0[i];
+            a[2 * (size_t)W * NF + w * NF + i] = worlds[w].qdd0[i];
+            a[3 * (size_t)W * NF + w * NF + i] = worlds[w].q_des[i];
+        }
+        if (O > 0) std::memcpy(&ob[(size_t)w * O * 12], worlds[w].obstacles, sizeof(double) * O * 12);
+    }
+    const size_t bytes = sizeof(double) * W * NF;
+    HIPCK(hipMemcpyAsync(p->q0, &a[0], bytes, hipMemcpyHostToDevice, p->stream));
+    HIPCK(hipMemcpyAsync(p->qd0, &a[(size_t)W * NF], bytes, hipMemcpyHostToDevice, p->stream));
+    HIPCK(hipMemcpyAsync(p->qdd0, &a[2 * (size_t)W * NF], bytes, hipMemcpyHostToDevice, p->stream));
+    HIPCK(hipMemcpyAsync(p->qdes, &a[3 * (size_t)W * NF], bytes, hipMemcpyHostToDevice, p->stream));
+    if (O > 0) HIPCK(hipMemcpyAsync(p->obs, ob.data(), sizeof(double) * ob.size(), hipMemcpyHostToDevice, p->stream));
+    HIPCK(hipStreamSynchronize(p->stream));  // host staging vectors die at return
+    p->W = W;
+    p->O = O;
+    NlpDev& d = p->d;
+    d.W = W;
+    d.O = O;
+    d.m = NF * p->T + p->T * p->NJ * O + NF * 4;
+    d.R = d.m + NF;
+    d.chunk = 2048;
+    d.nblk = (d.R + d.chunk - 1) / d.chunk;
+    return 0;
+}
+
+// reach set + hyperplanes + bounds for the uploaded batch
+static int run_reach(armour_planner* p) {
+    NlpDev& d = p->d;
+    ReachArgs ra = p->ra;
+    ra.W = p->W;
+    ra.T = p->T;
+    ra.q0 = p->q0;
+    ra.qd0 = p->qd0;
+    ra.qdd0 = p->qdd0;
+    HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, p->stream));
+    const long jobs = (long)p->W * p->T;
+    const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
+    hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, p->stream, p->d_rp, ra, p->ro);
+    HIPCK(hipGetLastError());
+    if (p->O > 0) {
+        const long planes = (long)p->W * p->T * p->NJ * p->O * COMB;
+        const int blocks = (int)((planes + 255) / 256 < 65535 * 4 ? (planes + 255) / 256 : 65535 * 4);
+        hipLaunchKernelGGL(hyperplane_kernel, dim3(blocks), dim3(256), 0, p->stream, d);
+        HIPCK(hipGetLastError());
+    }
+    const long rows = (long)p->W * d.R;
+    hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, p->stream, d);
+    HIPCK(hipGetLastError());
+    std::vector<int> err(p->W);
+    HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipStreamSynchronize(p->stream));
+    for (int w = 0; w < p->W; w++)
+        if (err[w]) {
+            char buf[160];
+            std::snprintf(buf, sizeof(buf), "reach-set job of world %d exceeded a capacity (error bits 0x%x)", w, err[w]);
+            return fail(ARMOUR_E_CAPACITY, buf);
+        }
+    p->reached = true;
+    return 0;
+}
+
+static int nside_count(const armour_planner* p) {
+    // finite constraint sides: torque 2/row, collision 1/row, extrema 2/row, box 2/variable
+    return 2 * NF * p->T + p->T * p->NJ * p->O + 2 * 4 * NF + 2 * NF;
+}
+
+static int run_solver(armour_planner* p) {
+    NlpDev& d = p->d;
+    const int W = p->W;
+    const dim3 rows(d.nblk, W), evg(p->T, W);
+    const int wb = (W + 63) / 64;
+    hipLaunchKernelGGL(ipm_world_init, dim3(wb), dim3(64), 0, p->stream, d);
+    hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 0);
+    hipLaunchKernelGGL(ipm_rows_init, rows, dim3(ROW_THREADS), 0, p->stream, d);
+    HIPCK(hipGetLastError());
+    const int ns = nside_count(p);
+    for (int it = 0; it <= d.opt.max_iter; it++) {
+        hipLaunchKernelGGL(ipm_rows_A, rows, dim3(ROW_THREADS), 0, p->stream, d);
+        hipLaunchKernelGGL(ipm_world_A, dim3(wb), dim3(64), 0, p->stream, d, ns);
+        hipLaunchKernelGGL(ipm_rows_B, rows, dim3(ROW_THREADS), 0, p->stream, d);
+        hipLaunchKernelGGL(ipm_world_B, dim3(wb), dim3(64), 0, p->stream, d);
+        for (int ls = 0; ls < d.opt.max_ls; ls++) {
+            HIPCK(hipMemsetAsync(d.flags, 0, sizeof(int), p->stream));
+            hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 1);
+            hipLaunchKernelGGL(ipm_rows_C, rows, dim3(ROW_THREADS), 0, p->stream, d);
+            hipLaunchKernelGGL(ipm_world_C, dim3(wb), dim3(64), 0, p->stream, d);
+            HIPCK(hipMemcpyAsync(p->h_flags, d.flags, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+            HIPCK(hipStreamSynchronize(p->stream));
+            if (p->h_flags[0] == 0) break;
+        }
+        HIPCK(hipMemsetAsync(d.flags + 1, 0, sizeof(int), p->stream));
+        hipLaunchKernelGGL(ipm_rows_D, rows, dim3(ROW_THREADS), 0, p->stream, d);
+        hipLaunchKernelGGL(ipm_world_D, dim3(wb), dim3(64), 0, p->stream, d);
+        HIPCK(hipGetLastError());
+        HIPCK(hipMemcpyAsync(p->h_flags + 1, d.flags + 1, sizeof(int), hipMemcpyDeviceToHost, p->stream));
+        HIPCK(hipStreamSynchronize(p->stream));
+        if (p->h_flags[1] == 0) break;  // every world converged, hit the cap or failed
+    }
+    hipLaunchKernelGGL(feasible_kernel, dim3(W), dim3(256), 0, p->stream, d, p->feas);
+    HIPCK(hipGetLastError());
+    return 0;
+}
+
+extern "C" {
+
+const char* armour_last_error(void) { return g_err.c_str(); }
+
+armour_planner* armour_create(const armour_config* cfg) {
+    if (!cfg) { fail(ARMOUR_E_ARG, "null config"); return nullptr; }
+    armour_planner* p = new armour_planner();
+    if (planner_init(p, cfg) != 0) {
+        std::string keep = g_err;
+        armour_destroy(p);
+        g_err = keep;
+        return nullptr;
+    }
+    return p;
+}
+
+void armour_destroy(armour_planner* p) {
+    if (!p) return;
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
+    for (void* a : p->allocs) (void)hipFree(a);
+    if (p->h_flags) (void)hipHostFree(p->h_flags);
+    if (p->h_ws) (void)hipHostFree(p->h_ws);
+    if (p->h_f) (void)hipHostFree(p->h_f);
+    if (p->h_feas) (void)hipHostFree(p->h_feas);
+    if (p->stream) {
+        for (int i = 0; i < 4; i++) (void)hipEventDestroy(p->ev[i]);
+        (void)hipStreamDestroy(p->stream);
+    }
+    delete p;
+}
+
+int armour_num_constraints(const armour_planner* p, int O) { return p ? NF * p->T + p->T * p->NJ * O + NF * 4 : ARMOUR_E_ARG; }
+int armour_num_joints(const armour_planner* p) { return p ? p->NJ : ARMOUR_E_ARG; }
+
+int armour_reach_batch(armour_planner* p, int W, const armour_world* worlds, armour_timing* timing) {
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    p->reached = p->planned = false;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = upload_worlds(p, W, worlds);
+    if (rc) return rc;
+    HIPCK(hipEventRecord(p->ev[0], p->stream));
+    if ((rc = run_reach(p))) return rc;
+    HIPCK(hipEventRecord(p->ev[1], p->stream));
+    HIPCK(hipEventSynchronize(p->ev[1]));
+    if (timing) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, p->ev[0], p->ev[1]);
+        timing->reach_ms = ms;
+        timing->nlp_ms = 0;
+        timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return 0;
+}
+
+int armour_plan_batch(armour_planner* p, int W, const armour_world* worlds, armour_result* results, armour_timing* timing) {
+    if (!p || !results) return fail(ARMOUR_E_ARG, "null planner / results");
+    p->reached = p->planned = false;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = upload_worlds(p, W, worlds);
+    if (rc) return rc;
+    HIPCK(hipEventRecord(p->ev[0], p->stream));
+    if ((rc = run_reach(p))) return rc;
+    HIPCK(hipEventRecord(p->ev[1], p->stream));
+    if ((rc = run_solver(p))) return rc;
+    HIPCK(hipEventRecord(p->ev[2], p->stream));
+    HIPCK(hipMemcpyAsync(p->h_ws, p->d.ws, sizeof(WorldState) * W, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipMemcpyAsync(p->h_f, p->d.f, sizeof(double) * 2 * p->Wmax, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipMemcpyAsync(p->h_feas, p->feas, sizeof(int) * W, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipStreamSynchronize(p->stream));
+    for (int w = 0; w < W; w++) {
+        const WorldState& S = p->h_ws[w];
+        armour_result& r = results[w];
+        for (int i = 0; i < NF; i++) r.k_opt[i] = S.x[i];
+        r.feasible = p->h_feas[w];
+        r.solver_status = S.status == 1 ? 0 : S.status == 2 ? 1 : 2;
+        r.iterations = S.iter;
+        r.evaluations = S.nevals;
+        r.cost = p->h_f[S.cur * p->d.W + w] / p->rp.cost_scale;
+        r.kkt_error = S.kkt;
+    }
+    p->planned = true;
+    if (timing) {
+        float a = 0, b = 0;
+        (void)hipEventElapsedTime(&a, p->ev[0], p->ev[1]);
+        (void)hipEventElapsedTime(&b, p->ev[1], p->ev[2]);
+        timing->reach_ms = a;
+        timing->nlp_ms = b;
+        timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return 0;
+}
+
+int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g, double* jac) {
+    if (!p || !x || !g) return fail(ARMOUR_E_ARG, "null argument");
+    if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set: call armour_reach_batch or armour_plan_batch first");
+    if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
+    NlpDev& d = p->d;
+    // evaluate every world of the batch at x in slot 0 (ws.x is the solver's start/end point, so
+    // a subsequent query of solver outputs must re-plan)
+    std::vector<WorldState> ws(p->W);
+    HIPCK(hipMemcpy(ws.data(), d.ws, sizeof(WorldState) * p->W, hipMemcpyDeviceToHost));
+    for (int i = 0; i < p->W; i++) {
+        for (int j = 0; j < NF; j++) ws[i].x[j] = x[j];
+        ws[i].status = 0;
+        ws[i].cur = 0;
+    }
+    HIPCK(hipMemcpy(d.ws, ws.data(), sizeof(WorldState) * p->W, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(eval_kernel, dim3(p->T, p->W), dim3(EVAL_THREADS), 0, p->stream, d, 0);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpyAsync(g, d.g + gidx(d, 0, w, 0), sizeof(double) * d.m, hipMemcpyDeviceToHost, p->stream));
+    if (jac) HIPCK(hipMemcpyAsync(jac, d.J + gidx(d, 0, w, 0) * NF, sizeof(double) * d.m * NF, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipStreamSynchronize(p->stream));
+    p->planned = false;
+    return 0;
+}
+
+int armour_get_constraints(armour_planner* p, int w, double* g) {
+    if (!p || !g) return fail(ARMOUR_E_ARG, "null argument");
+    if (!p->planned) return fail(ARMOUR_E_STATE, "no plan");
+    if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
+    const int cur = p->h_ws[w].cur;
+    HIPCK(hipMemcpy(g, p->d.g + gidx(p->d, cur, w, 0), sizeof(double) * p->d.m, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int armour_get_link_centers(armour_planner* p, int w, double* c) {
+    if (!p || !c) return fail(ARMOUR_E_ARG, "null argument");
+    if (!p->planned) return fail(ARMOUR_E_STATE, "no plan");
+    if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
+    HIPCK(hipMemcpy(c, p->d.link_c + (size_t)w * p->T * p->NJ * 3, sizeof(double) * p->T * p->NJ * 3, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int armour_get_link_generators(armour_planner* p, int w, double* gens) {
+    if (!p || !gens) return fail(ARMOUR_E_ARG, "null argument");
+    if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
+    if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
+    const size_t n = (size_t)p->T * p->NJ;
+    std::vector<double> cm(n * 18);
+    HIPCK(hipMemcpy(cm.data(), p->ro.link_gens + (size_t)w * n * 18, sizeof(double) * n * 18, hipMemcpyDeviceToHost));
+    for (size_t j = 0; j < n; j++)
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 6; c++) gens[j * 18 + r * 6 + c] = cm[j * 18 + r + 3 * c];
+    return 0;
+}
+
+int armour_get_torque_radius(armour_planner* p, int w, double* radius) {
+    if (!p || !radius) return fail(ARMOUR_E_ARG, "null argument");
+    if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
+    if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
+    HIPCK(hipMemcpy(radius, p->ro.torque_radius + (size_t)w * p->T * NF, sizeof(double) * p->T * NF, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+}  // extern "C"

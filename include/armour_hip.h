@@ -1,0 +1,100 @@
+/* armour_hip.h — C ABI of the MI355X-native ARMOUR planner (libarmour_hip.so).
+ *
+ * Drop-in boundary. The reference exposes its hot path to MATLAB as a process
+ * (KPR/armour_main.cu:12-400) driven through text files by KSI/uarmtd_planner.m:167-230; there is
+ * no mex entry. This library is what that process becomes: one call plans a batch of worlds on a
+ * GPU, each world being exactly one armour.in (KPR/README.md:99-112, armour_main.cu:54-77), each
+ * result exactly one armour*.out set (armour_main.cu:319-398). The drop-in executable
+ * `armour_main` (armour-dev_amd/csrc/armour_main.cpp) speaks the file protocol on top of it.
+ *
+ * Plain C types only; caller-owned inputs and outputs; one planner handle per thread.
+ * Every function returns 0 on success or a negative ARMOUR_E_* code; armour_last_error() gives
+ * the message (thread-local).
+ */
+#ifndef ARMOUR_HIP_H
+#define ARMOUR_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ARMOUR_NUM_FACTORS 7      /* NUM_FACTORS (KPR/KinovaWithoutGripperInfo.h:14) */
+#define ARMOUR_OBSTACLE_DOUBLES 12 /* center + 3 generators (armour_main.cu:45, uarmtd_planner.m:189) */
+
+enum {
+    ARMOUR_OK = 0,
+    ARMOUR_E_ARG = -1,       /* invalid argument (sizes, null pointers) */
+    ARMOUR_E_HIP = -2,       /* HIP runtime error / no device */
+    ARMOUR_E_CAPACITY = -3,  /* a reach-set job exceeded its arena / sort / output capacity */
+    ARMOUR_E_STATE = -4      /* query before a plan / reach call */
+};
+
+typedef struct armour_planner armour_planner;
+
+typedef struct armour_config {
+    int robot;           /* 0: Kinova Gen3 without gripper (KPR/KinovaWithoutGripperInfo.h) */
+    int num_time_steps;  /* NUM_TIME_STEPS (KPR/Parameters.h:17), runtime here, must be even */
+    int max_obstacles;   /* per world; MAX_OBSTACLE_NUM (KPR/Parameters.h:26) is 40 */
+    int max_worlds;      /* batch capacity */
+    int device;          /* HIP device ordinal (-1: current device) */
+    int max_iter;        /* solver iteration cap (0: default 100) */
+} armour_config;
+
+/* one planning problem: the content of armour.in */
+typedef struct armour_world {
+    double q0[ARMOUR_NUM_FACTORS];
+    double qd0[ARMOUR_NUM_FACTORS];
+    double qdd0[ARMOUR_NUM_FACTORS];
+    double q_des[ARMOUR_NUM_FACTORS];
+    int num_obstacles;
+    const double* obstacles; /* [num_obstacles][12] */
+} armour_world;
+
+/* one planning result: armour.out (k_opt or infeasible) + solver statistics */
+typedef struct armour_result {
+    double k_opt[ARMOUR_NUM_FACTORS]; /* normalised, in [-1, 1] (MATLAB scales by pi/48) */
+    int feasible;        /* finalize_solution re-check (KPR/NLPclass.cu:449-538) */
+    int solver_status;   /* 0 converged, 1 iteration cap, 2 line-search failure */
+    int iterations;
+    int evaluations;
+    double cost;         /* objective / COST_FUNCTION_OPTIMALITY_SCALE at k_opt */
+    double kkt_error;
+} armour_result;
+
+/* timings of the last batch, device-side (hipEvents on the planner's stream), milliseconds */
+typedef struct armour_timing {
+    double reach_ms;     /* JRS + PZ FK/RNEA + torque radius + hyperplanes */
+    double nlp_ms;       /* solver */
+    double total_ms;     /* incl. host<->device copies of inputs and results */
+} armour_timing;
+
+armour_planner* armour_create(const armour_config* cfg);
+void armour_destroy(armour_planner* p);
+const char* armour_last_error(void);
+
+/* constraints of a world with O obstacles: 7T + 7*T*O + 28  (KPR/NLPclass.cu:47-49) */
+int armour_num_constraints(const armour_planner* p, int num_obstacles);
+
+/* Plan a batch (all worlds must carry the same number of obstacles). Replaces
+ * armour_main.cu:87-316 for each world. */
+int armour_plan_batch(armour_planner* p, int num_worlds, const armour_world* worlds, armour_result* results,
+                      armour_timing* timing);
+
+/* Reach-set half only (armour_main.cu:87-222) for a batch; enables armour_eval_constraints. */
+int armour_reach_batch(armour_planner* p, int num_worlds, const armour_world* worlds, armour_timing* timing);
+
+/* eval_g / eval_jac_g (KPR/NLPclass.cu:272-396) of world w of the last batch at x; jac (m x 7,
+ * row-major) may be null. The parity-pinning entry. */
+int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g, double* jac);
+
+/* Outputs of world w of the last batch (the armour_*.out payloads, armour_main.cu:340-398) */
+int armour_get_constraints(armour_planner* p, int w, double* g);              /* m values at k_opt */
+int armour_get_link_centers(armour_planner* p, int w, double* centers);       /* [T][NJ][3] sliced */
+int armour_get_link_generators(armour_planner* p, int w, double* gens);       /* [T][NJ][3][6] */
+int armour_get_torque_radius(armour_planner* p, int w, double* radius);       /* [T][7] */
+int armour_num_joints(const armour_planner* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

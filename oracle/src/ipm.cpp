@@ -164,8 +164,14 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
         }
         double dx[NMAX];
         {
+            // inertia correction: shift the diagonal until the factorisation succeeds (bounded)
             double shift = 0.0;
-            while (!chol_solve(M, n, shift, rhs, dx)) shift = (shift == 0.0) ? 1e-8 : shift * 10;
+            bool ok = false;
+            for (int tries = 0; tries < 40 && !ok; tries++) {
+                ok = chol_solve(M, n, shift, rhs, dx);
+                shift = (shift == 0.0) ? 1e-8 : shift * 10;
+            }
+            if (!ok) { res.status = 2; break; }
         }
         // 4. step components and fraction to boundary
         const double tau = std::max(opt.tau_min, 1.0 - mu);

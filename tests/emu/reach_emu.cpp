@@ -1,0 +1,56 @@
+// TEST HARNESS — sequential host emulation of the reach kernel's workgroup program
+// (armour-dev_amd/csrc/reach.h) with a 1-thread group. Used only by tests/ to check the GPU
+// algorithm against the CPU oracle without a GPU; never part of the product library.
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include "reach.h"
+#include "robots.h"
+
+using namespace armour;
+
+extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, const double* qdd0,
+                         double* link_gens, double* link_center, double* link_rad, int* link_cnt,
+                         uint16_t* link_hash, double* link_coef, double* tq_center, double* tq_rad,
+                         int* tq_cnt, uint16_t* tq_hash, double* tq_coef, double* torque_radius,
+                         long* arena_used) {
+    static RobotParams rp;
+    static bool init = false;
+    if (!init) { kinova_gen3(rp); init = true; }
+    const long cap = 1 << 22;
+    std::vector<uint64_t> ah(cap);
+    std::vector<double> ac(cap * 3);
+    std::vector<PZH> H(hs::COUNT);
+    const int kcap = 1 << 16;
+    std::vector<uint64_t> kh(kcap);
+    std::vector<uint32_t> ki(kcap);
+    std::vector<int> kp(kcap);
+    double red[9 * 4];
+    int iscan[2];
+    Arena A{ah.data(), ac.data(), cap, cap * 3, 0, 0};
+    int err = 0;
+    Ctx x;
+    x.g = Grp{0, 1};
+    x.H = H.data();
+    x.opa = hs::OPA; x.opb = hs::OPB; x.opc = hs::OPC;
+    x.A = &A;
+    x.kh = kh.data(); x.ki = ki.data(); x.kp = kp.data(); x.cap_lds = kcap;
+    x.gkh = kh.data(); x.gki = ki.data(); x.gkp = kp.data(); x.cap_glb = kcap;
+    x.red = red;
+    x.iscan = iscan;
+    x.err = &err;
+    x.thr = rp.simplify_threshold;
+    int werr = 0;
+    ReachOut out;
+    out.T = 1;
+    out.NJ = rp.num_joints;
+    out.link_hash = link_hash; out.link_coef = link_coef; out.link_cnt = link_cnt;
+    out.link_center = link_center; out.link_rad = link_rad; out.link_gens = link_gens;
+    out.tq_hash = tq_hash; out.tq_coef = tq_coef; out.tq_cnt = tq_cnt; out.tq_center = tq_center;
+    out.tq_rad = tq_rad; out.torque_radius = torque_radius; out.err = &werr;
+    JrsJoint jrs[NF];
+    double scratch[2 * NF];
+    reach_job(x, rp, T, t, q0, qd0, qdd0, out, 0, jrs, scratch);
+    *arena_used = A.hused;
+    return err;
+}
