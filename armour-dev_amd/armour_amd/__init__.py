@@ -42,7 +42,11 @@ class Result(ctypes.Structure):
 
 
 class Timing(ctypes.Structure):
-    _fields_ = [("reach_ms", ctypes.c_double), ("nlp_ms", ctypes.c_double), ("total_ms", ctypes.c_double)]
+    _fields_ = [("reach_ms", ctypes.c_double), ("nlp_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("reach_kernel_ms", ctypes.c_double), ("reach_bytes", ctypes.c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 def lib():
@@ -61,6 +65,9 @@ def lib():
                                         ctypes.POINTER(Timing)]
         L.armour_reach_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Timing)]
         L.armour_eval_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
+        L.armour_get_reach_program.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.armour_get_reach_dump.argtypes = [ctypes.c_void_p, _dp, ctypes.c_int]
+        L.armour_get_reach_profile.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
         for name in ("armour_get_constraints", "armour_get_link_centers", "armour_get_link_generators",
                      "armour_get_torque_radius"):
             getattr(L, name).argtypes = [ctypes.c_void_p, ctypes.c_int, _dp]
@@ -72,7 +79,8 @@ def lib():
 ABI_SYMBOLS = ["armour_create", "armour_destroy", "armour_last_error", "armour_num_constraints",
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
-               "armour_num_joints"]
+               "armour_num_joints", "armour_get_reach_program", "armour_get_reach_profile",
+               "armour_get_reach_dump"]
 
 
 def _check(rc):
@@ -132,13 +140,13 @@ class Planner:
         for r in res:
             out.append(dict(k_opt=np.array(r.k_opt[:]), feasible=bool(r.feasible), status=r.solver_status,
                             iterations=r.iterations, evaluations=r.evaluations, cost=r.cost, kkt=r.kkt_error))
-        return out, dict(reach_ms=tm.reach_ms, nlp_ms=tm.nlp_ms, total_ms=tm.total_ms)
+        return out, tm.as_dict()
 
     def reach(self, worlds):
         arr = self._worlds(worlds)
         tm = Timing()
         _check(lib().armour_reach_batch(self.h, len(worlds), arr, ctypes.byref(tm)))
-        return dict(reach_ms=tm.reach_ms, total_ms=tm.total_ms)
+        return tm.as_dict()
 
     def eval_constraints(self, w, x, jac=True):
         m = self.num_constraints(self.O)
@@ -163,6 +171,33 @@ class Planner:
         g = np.zeros((self.T, self.NJ, 3, 6))
         _check(lib().armour_get_link_generators(self.h, w, _ptr(g)))
         return g
+
+    def reach_program(self):
+        """op codes of the reach kernel's program (diagnostics)"""
+        n = lib().armour_get_reach_program(self.h, None, 0)
+        codes = (ctypes.c_int * n)()
+        lib().armour_get_reach_program(self.h, codes, n)
+        return np.array(codes[:])
+
+    def reach_dump(self):
+        """[nops, 8] op-by-op state of job 0; needs ARMOUR_DUMP_OPS at creation"""
+        n = lib().armour_get_reach_dump(self.h, None, 0)
+        if n < 0:
+            _check(n)
+        d = np.zeros((n, 8))
+        _check(min(0, lib().armour_get_reach_dump(self.h, _ptr(d), n)))
+        return d
+
+    def reach_profile(self):
+        """([nops, 2] accumulated (cycles, terms) per op, [8] large-op phase cycles);
+        needs ARMOUR_PROFILE_OPS at creation"""
+        n = lib().armour_get_reach_profile(self.h, None, 0)
+        if n < 0:
+            _check(n)
+        buf = (ctypes.c_ulonglong * (2 * n + 8))()
+        _check(min(0, lib().armour_get_reach_profile(self.h, buf, n + 4)))
+        a = np.array(buf[:], dtype=np.uint64)
+        return a[:2 * n].reshape(n, 2), a[2 * n:]
 
     def torque_radius(self, w):
         r = np.zeros((self.T, NF))

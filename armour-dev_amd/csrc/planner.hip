@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -46,7 +47,14 @@ struct armour_planner {
     RobotParams rp;
     RobotParams* d_rp = nullptr;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4];
+    hipEvent_t ev[6];
+    // reach program (ProgramBuilder::ops) on the device
+    Op* d_prog = nullptr;
+    int nops = 0, nslots = 0;
+    unsigned long long* d_bytes = nullptr;
+    unsigned long long* d_prof = nullptr;  // per-op [cycles, terms] when ARMOUR_PROFILE_OPS is set
+    double* d_dump = nullptr;              // op-by-op state of job 0 when ARMOUR_DUMP_OPS is set
+    double last_kernel_ms = 0, last_bytes = 0;
     // inputs
     double *q0 = nullptr, *qd0 = nullptr, *qdd0 = nullptr, *qdes = nullptr, *obs = nullptr, *xin = nullptr;
     // reach
@@ -90,7 +98,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     p->Omax = cfg->max_obstacles;
     p->Wmax = cfg->max_worlds;
     HIPCK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-    for (int i = 0; i < 4; i++) HIPCK(hipEventCreate(&p->ev[i]));
+    for (int i = 0; i < 6; i++) HIPCK(hipEventCreate(&p->ev[i]));
     const int T = p->T, NJ = p->NJ, Om = p->Omax > 0 ? p->Omax : 1, Wm = p->Wmax;
     int rc = 0;
     if ((rc = p->alloc(&p->d_rp, 1))) return rc;
@@ -112,9 +120,34 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
         (rc = p->alloc(&ro.tq_rad, jobs * NF)) || (rc = p->alloc(&ro.torque_radius, jobs * NF)) ||
         (rc = p->alloc(&ro.err, (size_t)Wm)))
         return rc;
+    // reach program
+    {
+        ProgramBuilder pb;
+        pb.build(p->rp);
+        if (pb.nslots > MAX_SLOTS) return fail(ARMOUR_E_CAPACITY, "reach program needs more handle slots than MAX_SLOTS");
+        p->nops = (int)pb.ops.size();
+        p->nslots = pb.nslots;
+        if ((rc = p->alloc(&p->d_prog, pb.ops.size())) || (rc = p->alloc(&p->d_bytes, 1))) return rc;
+        HIPCK(hipMemcpy(p->d_prog, pb.ops.data(), sizeof(Op) * pb.ops.size(), hipMemcpyHostToDevice));
+        if (std::getenv("ARMOUR_PROFILE_OPS")) {
+            if ((rc = p->alloc(&p->d_prof, 2 * pb.ops.size() + 8))) return rc;
+            HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 8)));
+        }
+    }
     // reach workspace: two resident workgroups per CU, each with a private arena
     p->reach_grid = 2 * p->ncu;
     ReachArgs& ra = p->ra;
+    ra.prog = p->d_prog;
+    ra.nops = p->nops;
+    ra.bytes = p->d_bytes;
+    ra.prof = p->d_prof;
+    ra.mode = std::getenv("ARMOUR_ENGINE_MODE") ? std::atoi(std::getenv("ARMOUR_ENGINE_MODE")) : 0;
+    ra.dump = nullptr;
+    if (std::getenv("ARMOUR_DUMP_OPS")) {
+        if ((rc = p->alloc(&p->d_dump, (size_t)p->nops * DUMP_W))) return rc;
+        HIPCK(hipMemset(p->d_dump, 0, sizeof(double) * p->nops * DUMP_W));
+        ra.dump = p->d_dump;
+    }
     ra.arena_cap = 1 << 17;
     ra.gcap = 1 << 15;
     if ((rc = p->alloc(&ra.arena_h, (size_t)p->reach_grid * ra.arena_cap)) ||
@@ -203,10 +236,13 @@ static int run_reach(armour_planner* p) {
     ra.qd0 = p->qd0;
     ra.qdd0 = p->qdd0;
     HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, p->stream));
+    HIPCK(hipMemsetAsync(p->d_bytes, 0, sizeof(unsigned long long), p->stream));
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
+    HIPCK(hipEventRecord(p->ev[3], p->stream));
     hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, p->stream, p->d_rp, ra, p->ro);
     HIPCK(hipGetLastError());
+    HIPCK(hipEventRecord(p->ev[4], p->stream));
     if (p->O > 0) {
         const long planes = (long)p->W * p->T * p->NJ * p->O * COMB;
         const int blocks = (int)((planes + 255) / 256 < 65535 * 4 ? (planes + 255) / 256 : 65535 * 4);
@@ -217,8 +253,16 @@ static int run_reach(armour_planner* p) {
     hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, p->stream, d);
     HIPCK(hipGetLastError());
     std::vector<int> err(p->W);
+    unsigned long long bytes = 0;
     HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipMemcpyAsync(&bytes, p->d_bytes, sizeof(bytes), hipMemcpyDeviceToHost, p->stream));
     HIPCK(hipStreamSynchronize(p->stream));
+    {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, p->ev[3], p->ev[4]);
+        p->last_kernel_ms = ms;
+        p->last_bytes = (double)bytes;
+    }
     for (int w = 0; w < p->W; w++)
         if (err[w]) {
             char buf[160];
@@ -296,7 +340,7 @@ void armour_destroy(armour_planner* p) {
     if (p->h_f) (void)hipHostFree(p->h_f);
     if (p->h_feas) (void)hipHostFree(p->h_feas);
     if (p->stream) {
-        for (int i = 0; i < 4; i++) (void)hipEventDestroy(p->ev[i]);
+        for (int i = 0; i < 6; i++) (void)hipEventDestroy(p->ev[i]);
         (void)hipStreamDestroy(p->stream);
     }
     delete p;
@@ -320,6 +364,8 @@ int armour_reach_batch(armour_planner* p, int W, const armour_world* worlds, arm
         (void)hipEventElapsedTime(&ms, p->ev[0], p->ev[1]);
         timing->reach_ms = ms;
         timing->nlp_ms = 0;
+        timing->reach_kernel_ms = p->last_kernel_ms;
+        timing->reach_bytes = p->last_bytes;
         timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return 0;
@@ -358,6 +404,8 @@ int armour_plan_batch(armour_planner* p, int W, const armour_world* worlds, armo
         (void)hipEventElapsedTime(&b, p->ev[1], p->ev[2]);
         timing->reach_ms = a;
         timing->nlp_ms = b;
+        timing->reach_kernel_ms = p->last_kernel_ms;
+        timing->reach_bytes = p->last_bytes;
         timing->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return 0;
@@ -423,6 +471,32 @@ int armour_get_torque_radius(armour_planner* p, int w, double* radius) {
     if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
     HIPCK(hipMemcpy(radius, p->ro.torque_radius + (size_t)w * p->T * NF, sizeof(double) * p->T * NF, hipMemcpyDeviceToHost));
     return 0;
+}
+
+int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms, int capacity) {
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    if (!p->d_prof) return fail(ARMOUR_E_STATE, "op profiling is off (set ARMOUR_PROFILE_OPS before armour_create)");
+    if (cycles_terms && capacity >= p->nops + 4)
+        HIPCK(hipMemcpy(cycles_terms, p->d_prof, sizeof(unsigned long long) * (2 * p->nops + 8), hipMemcpyDeviceToHost));
+    return p->nops;
+}
+
+int armour_get_reach_dump(armour_planner* p, double* dump, int capacity) {
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    if (!p->d_dump) return fail(ARMOUR_E_STATE, "op dump is off (set ARMOUR_DUMP_OPS before armour_create)");
+    if (dump && capacity >= p->nops)
+        HIPCK(hipMemcpy(dump, p->d_dump, sizeof(double) * DUMP_W * p->nops, hipMemcpyDeviceToHost));
+    return p->nops;
+}
+
+int armour_get_reach_program(const armour_planner* p, int* codes, int capacity) {
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    if (codes && capacity >= p->nops) {
+        std::vector<Op> ops(p->nops);
+        HIPCK(hipMemcpy(ops.data(), p->d_prog, sizeof(Op) * p->nops, hipMemcpyDeviceToHost));
+        for (int k = 0; k < p->nops; k++) codes[k] = ops[k].code;
+    }
+    return p->nops;
 }
 
 }  // extern "C"

@@ -3,30 +3,42 @@
 // Semantics are those of the reference's PZsparse (KPR/PZsparse.cu:284-1167): monomials carry a
 // 63-bit degree hash, products add hashes without carry, and every operator ends in simplify():
 // merge equal hashes, prune merged coefficients whose Frobenius norm is <= SIMPLIFY_THRESHOLD
-// into the interval part `independent`. The data layout is MI355X-first:
-//   * a PZ is a handle (dims, centre, independent part) in LDS plus a structure-of-arrays run of
-//     monomials (hash[], coefficient block[]) in a per-workgroup HBM arena (bump allocated);
-//   * element extraction, scaling by a constant and negation are lazy views on a parent's
-//     monomials (no copies) — the reader applies s*c exactly as the reference's materialised copy;
-//   * simplify() is a bitonic sort of (hash, term-index) keys in LDS, a segmented group sum in
-//     term order, a norm test, and a block-wide scan/compaction into the arena;
+// into the interval part `independent`. The data layout and algorithms are MI355X-first:
+//   * a PZ is a handle (dims, centre, independent parts, sum|m_k|) in LDS plus a structure-of-
+//     arrays run of monomials (hash[], coefficient block[]) in a per-workgroup HBM arena (bump
+//     allocated). Every materialised run is sorted by hash with unique hashes (it is the output
+//     of a simplify), which the operators below exploit;
+//   * element extraction and scaling by a constant are lazy views on a parent's monomials (no
+//     copies) — the reader applies s*c exactly as the reference's materialised copy would;
+//   * simplify() orders (hash, term-index) keys and sums each equal-hash group in term order:
+//       - N <= 64 terms: wave 0 alone. Each lane loads its term (hash + coefficients, one memory
+//         round trip), a bitonic network over __shfl_xor sorts the keys in registers, the
+//         coefficients follow by ds_bpermute, groups are summed by shuffles and compacted with
+//         ballot/popcount — no LDS traffic and no workgroup barrier;
+//       - larger: the operands are first staged into LDS with coalesced loads; then the order is
+//         built either by RANK MERGE (operator+/-, stack, addOneDim and products with few runs:
+//         the term list is a union of sorted runs, each key's rank is the sum of its lower bounds
+//         in the other runs — no sort), or by a register bitonic sort (256 x E keys, stages with
+//         j < E in registers, j < 64E by wave shuffles, only 3 stages through LDS);
 //   * every PZ carries TWO independent parts (nominal / interval inertial parameters). The
 //     reference runs RNEA twice (armour_main.cu:129,132) with identical centres and monomials —
-//     only `independent` differs — so one pass with dual independent parts replaces both.
-// Operators stage their operand handles in dedicated LDS slots (opa/opb/opc) so that an output
-// may alias an input; coefficient blocks are fixed 9-element register arrays with unrolled loops.
+//     only `independent` differs — so one pass with dual independent parts replaces both;
+//   * each handle carries sum_k |m_k| (elementwise), so a product's independent part needs no
+//     pass over its operands' monomials.
+// All device functions are force-inlined: the reach kernel is an interpreter whose op bodies
+// are inlined once each into one switch (reach.h), so the program runs with no device calls.
 // The group abstraction (Grp) lets the same code run as a sequential host emulation in tests.
 #pragma once
 #include "common.h"
 
-#define ADN __host__ __device__ __attribute__((noinline))
+#define AI __host__ __device__ inline __attribute__((always_inline))
 #define UNR _Pragma("unroll")
 
 namespace armour {
 
 struct Grp {
     int tid, n;
-    AD void sync() const {
+    AI void sync() const {
 #if defined(__HIP_DEVICE_COMPILE__)
         __syncthreads();
 #endif
@@ -35,7 +47,7 @@ struct Grp {
 
 // PZ handle. Views: comp >= 0 selects one element of the parent's coefficient block (the
 // reference's operator()(r,c), PZsparse.cu:678-697); scaled applies s * c on read (PZ * double,
-// :996-1030); neg applies -c on read (the second operand of operator-, :813-834).
+// :996-1030).
 struct PZH {
     int R, C;
     int cnt;
@@ -43,11 +55,10 @@ struct PZH {
     long hoff, coff;
     int comp;
     int scaled;
-    int neg;
-    int pad_;
     double scale;
     double center[9];
     double ind[2][9];
+    double absum[9];  // sum_k |m_k| elementwise, as the handle presents its monomials
 };
 
 struct Arena {
@@ -55,71 +66,60 @@ struct Arena {
     double* c;
     long hcap, ccap;
     long hused, cused;
+    double bytes;  // algorithmic monomial bytes read + written by the operators of this job
 };
 
 struct Ctx {
     Grp g;
     PZH* H;            // handle table (LDS)
-    int opa, opb, opc; // operand staging slots in H
     Arena* A;          // bump arena state (LDS), storage in HBM
-    uint64_t* kh;      // sort keys: hash        (LDS, cap_lds entries)
-    uint32_t* ki;      // sort keys: term index
+    uint64_t* kh;      // ordered keys: hash        (LDS, cap_lds entries)
+    uint32_t* ki;      // ordered keys: term index
     int* kp;           // keep flags / scan
     int cap_lds;
-    uint64_t* gkh;     // global fallback for large sorts
+    uint64_t* gkh;     // global fallback for large operators
     uint32_t* gki;
     int* gkp;
     int cap_glb;
-    double* red;       // reduction scratch (LDS): [waves * 9] on device, [n * 9] in the emulation
-    int* iscan;        // [2 * n] scan scratch (LDS)
+    double* stage;     // operand staging (LDS), stage_cap doubles
+    int stage_cap;
+    double* red;       // reduction scratch (LDS): [waves * 18] on device, [n * 18] in the emulation
+    int* iscan;        // scan scratch (LDS): [waves] on device, [2 * n] in the emulation
     int* err;          // error word (LDS)
     double thr;
+    unsigned long long* phase;  // optional large-operator phase cycle counters [8] (profiling)
+    int mode;          // diagnostics: bit 0 = no wave-0 path, bit 1 = no register sort (rank merge)
 };
 
 enum : int { ERR_ARENA = 1, ERR_SORTCAP = 2, ERR_LINKGEN = 4, ERR_OUTCAP = 8, ERR_HANDLES = 16 };
 
 // ---------------------------------------------------------------------------------------------
 // scalar helpers (fixed 9-element blocks, unrolled so blocks stay in registers)
-template <int N>
-AD double frob_norm_n(const double* x) {
+AI double frob_norm(const double* x, int n) {
     // Eigen 3.3 MatrixXd::norm(): packet-of-2 redux order (same as oracle/src/pz.cpp)
-    if (N == 1) return sqrt(x[0] * x[0]);
-    if (N == 3) return sqrt((x[0] * x[0] + x[1] * x[1]) + x[2] * x[2]);
+    if (n == 1) return sqrt(x[0] * x[0]);
+    if (n == 3) return sqrt((x[0] * x[0] + x[1] * x[1]) + x[2] * x[2]);
     const double s0 = x[0] * x[0], s1 = x[1] * x[1], s2 = x[2] * x[2], s3 = x[3] * x[3], s4 = x[4] * x[4];
     const double s5 = x[5] * x[5], s6 = x[6] * x[6], s7 = x[7] * x[7], s8 = x[8] * x[8];
     return sqrt((((s0 + s4) + (s2 + s6)) + ((s1 + s5) + (s3 + s7))) + s8);
 }
-AD double frob_norm(const double* x, int n) {
-    return n == 1 ? frob_norm_n<1>(x) : n == 3 ? frob_norm_n<3>(x) : frob_norm_n<9>(x);
+
+// column-major coefficient-based product, inner index summed in order. The program only forms
+// (3x3)(3x3) and (3x3)(3x1) block products (1x1 operands are handled as scalings); any other
+// shape is flagged by the caller.
+AI void matmul(const double* A, int ra, int ca, const double* B, int cb, double* out) {
+    double t[9];
+    UNR for (int e = 0; e < 9; e++) t[e] = 0.0;
+    UNR for (int j = 0; j < 3; j++)
+        UNR for (int i = 0; i < 3; i++)
+            if (j < cb) t[i + 3 * j] = (A[i] * B[3 * j] + A[i + 3] * B[3 * j + 1]) + A[i + 6] * B[3 * j + 2];
+    UNR for (int e = 0; e < 9; e++) out[e] = t[e];
 }
 
-// column-major coefficient-based product, inner index summed in order; dims in {1,3}
-AD void matmul(const double* A, int ra, int ca, const double* B, int cb, double* out) {
-    if (ra == 3 && ca == 3 && cb == 1) {
-        double t[3];
-        UNR for (int i = 0; i < 3; i++) t[i] = (A[i] * B[0] + A[i + 3] * B[1]) + A[i + 6] * B[2];
-        UNR for (int i = 0; i < 3; i++) out[i] = t[i];
-    } else if (ra == 3 && ca == 3 && cb == 3) {
-        double t[9];
-        UNR for (int j = 0; j < 3; j++)
-            UNR for (int i = 0; i < 3; i++) t[i + 3 * j] = (A[i] * B[3 * j] + A[i + 3] * B[3 * j + 1]) + A[i + 6] * B[3 * j + 2];
-        UNR for (int e = 0; e < 9; e++) out[e] = t[e];
-    } else {
-        double t[9];
-        for (int j = 0; j < cb; j++)
-            for (int i = 0; i < ra; i++) {
-                double acc = A[i] * B[j * ca];
-                for (int k = 1; k < ca; k++) acc = acc + A[i + k * ra] * B[k + j * ca];
-                t[i + j * ra] = acc;
-            }
-        for (int e = 0; e < ra * cb; e++) out[e] = t[e];
-    }
-}
-
-AD int nel(const PZH& h) { return h.R * h.C; }
+AI int nel(const PZH& h) { return h.R * h.C; }
 
 // read monomial k of handle h into a 9-block (entries >= nel(h) are zero)
-AD void read_mono(const Ctx& x, const PZH& h, int k, double* out) {
+AI void read_mono(const Ctx& x, const PZH& h, int k, double* out) {
     const double* base = x.A->c + h.coff + (long)k * h.stride;
     const int n = nel(h);
     UNR for (int e = 0; e < 9; e++) {
@@ -127,52 +127,78 @@ AD void read_mono(const Ctx& x, const PZH& h, int k, double* out) {
         if (e < n) {
             v = base[h.comp >= 0 ? h.comp : e];
             if (h.scaled) v = h.scale * v;
-            if (h.neg) v = -v;
         }
         out[e] = v;
     }
 }
-AD uint64_t mono_hash(const Ctx& x, const PZH& h, int k) { return x.A->h[h.hoff + k]; }
+AI uint64_t mono_hash(const Ctx& x, const PZH& h, int k) { return x.A->h[h.hoff + k]; }
 
 // ---------------------------------------------------------------------------------------------
-// block primitives
-AD void block_sum9(const Ctx& x, double* v) {
-    // deterministic reduction of a 9-block over the group; result in v on every thread
+// wave / block primitives
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline __attribute__((always_inline)) double wsum(double v) {
+    UNR for (int m = 32; m > 0; m >>= 1) v = v + __shfl_xor(v, m, 64);
+    return v;
+}
+#endif
+
+// deterministic reduction of an n-block (n <= 18) over the group; result in v on every thread
+AI void block_sum(const Ctx& x, double* v, int n) {
     const Grp& g = x.g;
 #if defined(__HIP_DEVICE_COMPILE__)
-    // wave64 butterfly (every lane ends with the same sum), then the waves in order
-    UNR for (int e = 0; e < 9; e++)
-        UNR for (int m = 32; m > 0; m >>= 1) v[e] = v[e] + __shfl_xor(v[e], m, 64);
+    UNR for (int e = 0; e < 18; e++) if (e < n) v[e] = wsum(v[e]);
     const int wave = g.tid >> 6, nw = (g.n + 63) >> 6;
     if ((g.tid & 63) == 0)
-        UNR for (int e = 0; e < 9; e++) x.red[wave * 9 + e] = v[e];
+        UNR for (int e = 0; e < 18; e++) if (e < n) x.red[wave * 18 + e] = v[e];
     g.sync();
-    UNR for (int e = 0; e < 9; e++) {
-        double s = x.red[e];
-        for (int w = 1; w < nw; w++) s = s + x.red[w * 9 + e];
-        v[e] = s;
+    UNR for (int e = 0; e < 18; e++) {
+        if (e < n) {
+            double s = x.red[e];
+            for (int w = 1; w < nw; w++) s = s + x.red[w * 18 + e];
+            v[e] = s;
+        }
     }
     g.sync();
 #else
-    for (int e = 0; e < 9; e++) x.red[g.tid * 9 + e] = v[e];
+    for (int e = 0; e < n; e++) x.red[g.tid * 18 + e] = v[e];
     g.sync();
     for (int s = g.n / 2; s > 0; s >>= 1) {
         if (g.tid < s)
-            for (int e = 0; e < 9; e++) x.red[g.tid * 9 + e] = x.red[g.tid * 9 + e] + x.red[(g.tid + s) * 9 + e];
+            for (int e = 0; e < n; e++) x.red[g.tid * 18 + e] = x.red[g.tid * 18 + e] + x.red[(g.tid + s) * 18 + e];
         g.sync();
     }
-    for (int e = 0; e < 9; e++) v[e] = x.red[e];
+    for (int e = 0; e < n; e++) v[e] = x.red[e];
     g.sync();
 #endif
 }
 
-// exclusive scan of kp[0..N) in place; returns total
-AD int block_scan(const Ctx& x, int* kp, int N) {
+// exclusive scan of kp[0..N) in place (contiguous chunk per thread); returns total
+AI int block_scan(const Ctx& x, int* kp, int N) {
     const Grp& g = x.g;
     const int chunk = (N + g.n - 1) / g.n;
     const int lo = g.tid * chunk, hi = (lo + chunk < N) ? lo + chunk : N;
     int s = 0;
     for (int i = lo; i < hi; i++) s += kp[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int lane = g.tid & 63, wave = g.tid >> 6, nw = (g.n + 63) >> 6;
+    int inc = s;
+    UNR for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) x.iscan[wave] = inc;
+    g.sync();
+    int base = 0, total = 0;
+    for (int w = 0; w < nw; w++) {
+        const int t = x.iscan[w];
+        if (w < wave) base += t;
+        total += t;
+    }
+    int run = base + inc - s;
+    for (int i = lo; i < hi; i++) { const int v = kp[i]; kp[i] = run; run += v; }
+    g.sync();
+    return total;
+#else
     int* a = x.iscan;
     int* b = x.iscan + g.n;
     a[g.tid] = s;
@@ -188,12 +214,14 @@ AD int block_scan(const Ctx& x, int* kp, int N) {
     for (int i = lo; i < hi; i++) { const int v = kp[i]; kp[i] = run; run += v; }
     g.sync();
     return total;
+#endif
 }
 
-AD bool key_less(uint64_t h1, uint32_t i1, uint64_t h2, uint32_t i2) { return h1 < h2 || (h1 == h2 && i1 < i2); }
+AI bool key_less(uint64_t h1, uint32_t i1, uint64_t h2, uint32_t i2) { return h1 < h2 || (h1 == h2 && i1 < i2); }
 
-// bitonic sort of P (power of two) keys ascending by (hash, index)
-ADN void bitonic(const Ctx& x, uint64_t* kh, uint32_t* ki, int P) {
+// bitonic sort of P (power of two) keys in memory, whole group (host emulation and the global
+// fallback for operators beyond the LDS key capacity)
+AI void bitonic_mem(const Ctx& x, uint64_t* kh, uint32_t* ki, int P) {
     const Grp& g = x.g;
     for (int k = 2; k <= P; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
@@ -211,60 +239,441 @@ ADN void bitonic(const Ctx& x, uint64_t* kh, uint32_t* ki, int P) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// arena / handles. Convention: thread 0 stages operand handles into x.opa/opb/opc and writes the
-// output header (dims, centre, independent parts) into the shared table; after a sync every
-// thread reads handles from LDS; simplify_terms() then fills the output's monomials.
-
-AD void alloc_out(Ctx& x, int o, int K, int stride) {
-    if (x.g.tid == 0) {
-        PZH& h = x.H[o];
-        h.stride = stride;
-        if (x.A->hused + K > x.A->hcap || x.A->cused + (long)K * stride > x.A->ccap) {
-            *x.err |= ERR_ARENA;
-            h.cnt = 0; h.hoff = 0; h.coff = 0;
-        } else {
-            h.hoff = x.A->hused;
-            h.coff = x.A->cused;
-            h.cnt = K;
-            x.A->hused += K;
-            x.A->cused += (long)K * stride;
+// operands as the term generator sees them: a run of `cnt` monomials with hashes h[k] and
+// coefficient rows c[k * stride + (comp >= 0 ? comp : e)], e < n, times scale if scaled.
+struct Src {
+    const uint64_t* h;
+    const double* c;
+    int cnt, n, stride, comp, scaled;
+    double scale;
+    AI uint64_t hash(int k) const { return h[k]; }
+    AI void read(int k, bool neg, double* out) const {
+        const double* base = c + (long)k * stride;
+        UNR for (int e = 0; e < 9; e++) {
+            double v = 0.0;
+            if (e < n) {
+                v = base[comp >= 0 ? comp : e];
+                if (scaled) v = scale * v;
+                if (neg) v = -v;
+            }
+            out[e] = v;
         }
     }
-    x.g.sync();
+};
+
+AI Src src_of(const Ctx& x, const PZH& p) {
+    Src s;
+    s.h = x.A->h + p.hoff;
+    s.c = x.A->c + p.coff;
+    s.cnt = p.cnt;
+    s.n = nel(p);
+    s.stride = p.stride;
+    s.comp = p.comp;
+    s.scaled = p.scaled;
+    s.scale = p.scale;
+    return s;
 }
 
-AD void hdr_init(PZH& h, int R, int C) {
-    h.R = R; h.C = C; h.cnt = 0; h.stride = R * C; h.hoff = 0; h.coff = 0;
-    h.comp = -1; h.scaled = 0; h.neg = 0; h.scale = 1.0;
-    UNR for (int e = 0; e < 9; e++) { h.center[e] = 0.0; h.ind[0][e] = 0.0; h.ind[1][e] = 0.0; }
+// first k in [0, cnt) with h[k] >= key (runs are strictly increasing)
+AI int lower_bound(const uint64_t* h, int cnt, uint64_t key) {
+    int lo = 0, len = cnt;
+    while (len > 0) {
+        const int half = len >> 1;
+        if (h[lo + half] < key) { lo += half + 1; len -= half + 1; }
+        else len = half;
+    }
+    return lo;
+}
+// same over the T3 row i of a product: keys ha + hb[j]
+AI int lower_bound_off(const uint64_t* h, int cnt, uint64_t off, uint64_t key) {
+    int lo = 0, len = cnt;
+    while (len > 0) {
+        const int half = len >> 1;
+        if (off + h[lo + half] < key) { lo += half + 1; len -= half + 1; }
+        else len = half;
+    }
+    return lo;
+}
+// T3 column j of a product: keys ha[i] + hb_j over i
+AI int lower_bound_col(const uint64_t* ha, int cnt, uint64_t hbj, uint64_t key) { return lower_bound_off(ha, cnt, hbj, key); }
+
+// term lists of an operator: kind 0 = product (PZsparse.cu:864-994: T1 a_i x B.c, T2 A.c x b_j,
+// T3 a_i x b_j with hash a_i + b_j), kind 1 = concatenation of up to 3 sources, each a full block
+// (place = -1) or a 1x1 source placed at component `place` (operator+/-, stack, addOneDimPZ)
+struct Terms {
+    int kind, ns;
+    Src S[3];
+    int places;        // 4 bits per source: component + 1 (0: full block)
+    int negs;          // bit per source: negate on read
+    const double* Ac;  // product: operand centres (LDS handles)
+    const double* Bc;
+    int AR, AC, BC;
+    int nout;          // elements of the output block
+    AI void which(int p, int& s, int& k) const {
+        s = 0;
+        if (p >= S[0].cnt) { p -= S[0].cnt; s = 1; if (p >= S[1].cnt) { p -= S[1].cnt; s = 2; } }
+        k = p;
+    }
+    AI uint64_t hash(int p) const {
+        if (kind == 0) {
+            const int na = S[0].cnt, nb = S[1].cnt;
+            if (p < na) return S[0].hash(p);
+            if (p < na + nb) return S[1].hash(p - na);
+            const int q = p - na - nb;
+            return S[0].hash(q / nb) + S[1].hash(q % nb);
+        }
+        int s, k;
+        which(p, s, k);
+        return s == 0 ? S[0].hash(k) : s == 1 ? S[1].hash(k) : S[2].hash(k);
+    }
+    AI void prod(const double* a, const double* b, double* out) const {
+        const bool as = AR == 1 && AC == 1, bs = S[1].n == 1;
+        if (as) { UNR for (int e = 0; e < 9; e++) out[e] = a[0] * b[e]; }
+        else if (bs) { UNR for (int e = 0; e < 9; e++) out[e] = a[e] * b[0]; }
+        else matmul(a, AR, AC, b, BC, out);
+    }
+    AI void coef(int p, double* out) const {
+        if (kind == 0) {
+            const int na = S[0].cnt, nb = S[1].cnt;
+            double a[9], b[9];
+            if (p < na) {
+                S[0].read(p, false, a);
+                UNR for (int e = 0; e < 9; e++) b[e] = Bc[e];
+                prod(a, b, out);
+                return;
+            }
+            if (p < na + nb) {
+                S[1].read(p - na, false, b);
+                UNR for (int e = 0; e < 9; e++) a[e] = Ac[e];
+                prod(a, b, out);
+                return;
+            }
+            const int q = p - na - nb;
+            S[0].read(q / nb, false, a);
+            S[1].read(q % nb, false, b);
+            prod(a, b, out);
+            return;
+        }
+        int s, k;
+        which(p, s, k);
+        const bool ng = (negs >> s) & 1;
+        if (s == 0) S[0].read(k, ng, out);
+        else if (s == 1) S[1].read(k, ng, out);
+        else S[2].read(k, ng, out);
+        const int pl = ((places >> (4 * s)) & 15) - 1;
+        if (pl >= 0) {
+            const double v = out[0];
+            UNR for (int e = 0; e < 9; e++) out[e] = (e == pl) ? v : 0.0;
+        }
+    }
+    AI double in_bytes() const {
+        double b = 0;
+        UNR for (int s = 0; s < 3; s++) if (s < ns) b += (double)S[s].cnt * (8.0 + 8.0 * S[s].n);
+        return b;
+    }
+    // number of sorted runs the term list is made of (rank merge cost)
+    AI int runs() const {
+        if (kind == 1) return ns;
+        const int na = S[0].cnt, nb = S[1].cnt;
+        return 2 + (na < nb ? na : nb);
+    }
+    // rank of term p (hash h) in the (hash, term index) order of the whole list
+    AI int rank(int p, uint64_t h) const {
+        int r = 0;
+        if (kind == 1) {
+            int s, k;
+            which(p, s, k);
+            UNR for (int t = 0; t < 3; t++) {
+                if (t >= ns) continue;
+                if (t == s) { r += k; continue; }
+                int lb = lower_bound(S[t].h, S[t].cnt, h);
+                if (t < s && lb < S[t].cnt && S[t].h[lb] == h) lb++;
+                r += lb;
+            }
+            return r;
+        }
+        const int na = S[0].cnt, nb = S[1].cnt;
+        // T1: indices 0..na-1
+        {
+            int lb = lower_bound(S[0].h, na, h);
+            if (lb < na && S[0].h[lb] == h && lb < p) lb++;
+            r += lb;
+        }
+        // T2: indices na..na+nb-1
+        {
+            int lb = lower_bound(S[1].h, nb, h);
+            if (lb < nb && S[1].h[lb] == h && na + lb < p) lb++;
+            r += lb;
+        }
+        const int base = na + nb;
+        if (na <= nb) {
+            for (int i = 0; i < na; i++) {
+                const uint64_t hai = S[0].h[i];
+                int lb = lower_bound_off(S[1].h, nb, hai, h);
+                if (lb < nb && hai + S[1].h[lb] == h && base + i * nb + lb < p) lb++;
+                r += lb;
+            }
+        } else {
+            for (int j = 0; j < nb; j++) {
+                const uint64_t hbj = S[1].h[j];
+                int lb = lower_bound_col(S[0].h, na, hbj, h);
+                if (lb < na && S[0].h[lb] + hbj == h && base + lb * nb + j < p) lb++;
+                r += lb;
+            }
+        }
+        return r;
+    }
+};
+
+// copy the sources into LDS (hashes, then effective coefficient rows), if they fit; uniform
+// decision. The caller's barrier publishes the staged copy.
+AI void stage_sources(Ctx& x, Terms& T) {
+    int need = 0;
+    UNR for (int s = 0; s < 3; s++) if (s < T.ns) need += T.S[s].cnt * (1 + T.S[s].n);
+    if (need > x.stage_cap) return;
+    double* base = x.stage;
+    UNR for (int s = 0; s < 3; s++) {
+        if (s >= T.ns) continue;
+        Src& S = T.S[s];
+        uint64_t* hs = (uint64_t*)base;
+        double* cs = base + S.cnt;
+        for (int k = x.g.tid; k < S.cnt; k += x.g.n) {
+            hs[k] = S.h[k];
+            const double* src = S.c + (long)k * S.stride;
+            for (int e = 0; e < S.n; e++) {
+                double v = src[S.comp >= 0 ? S.comp : e];
+                if (S.scaled) v = S.scale * v;
+                cs[k * S.n + e] = v;
+            }
+        }
+        S.h = hs;
+        S.c = cs;
+        S.stride = S.n;
+        S.comp = -1;
+        S.scaled = 0;
+        S.scale = 1.0;
+        base += S.cnt * (1 + S.n);
+    }
 }
 
-// generic simplify over a term list (hash(p), coef(p)) into shared handle o, whose header
-// (dims, centre, independent parts: the operator's own formula) is already set; the pruned
-// amount is added to both independent parts as in PZsparse.cu:347-349.
-template <class Terms>
-ADN void simplify_terms(Ctx& x, int o, const Terms& T, int N) {
+AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
+    h.stride = stride;
+    if (x.A->hused + K > x.A->hcap || x.A->cused + (long)K * stride > x.A->ccap) {
+        *x.err |= ERR_ARENA;
+        h.cnt = 0; h.hoff = 0; h.coff = 0;
+    } else {
+        h.hoff = x.A->hused;
+        h.coff = x.A->cused;
+        h.cnt = K;
+        x.A->hused += K;
+        x.A->cused += (long)K * stride;
+    }
+}
+
+// output header finish (thread 0): pruned amount into both independent parts (PZsparse.cu:347-349)
+AI void finish_t0(PZH& h, const double* red, const double* abs, int n) {
+    if (frob_norm(red, n) != 0)
+        UNR for (int v = 0; v < 2; v++)
+            UNR for (int e = 0; e < 9; e++) if (e < n) h.ind[v][e] = h.ind[v][e] + red[e];
+    UNR for (int e = 0; e < 9; e++) h.absum[e] = e < n ? abs[e] : 0.0;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// ---- N <= 64: wave 0 alone, keys and coefficients in registers --------------------------------
+__device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int o, const Terms& T, int N) {
+    const int n = T.nout;
+    const int lane = x.g.tid & 63;
+    uint64_t h = ~(uint64_t)0;
+    double c[9];
+    if (lane < N) {
+        h = T.hash(lane);
+        T.coef(lane, c);
+    } else {
+        UNR for (int e = 0; e < 9; e++) c[e] = 0.0;
+    }
+    uint32_t id = (uint32_t)lane;
+    int P = 1;
+    while (P < N) P <<= 1;
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t oh = __shfl_xor(h, j, 64);
+            const uint32_t oi = __shfl_xor(id, j, 64);
+            const bool asc = (lane & k) == 0, lower = (lane & j) == 0;
+            const bool other_less = key_less(oh, oi, h, id);
+            if ((lower == asc) ? other_less : !other_less) { h = oh; id = oi; }
+        }
+    // coefficients follow their keys
+    UNR for (int e = 0; e < 9; e++) if (e < n) c[e] = __shfl(c[e], (int)id, 64);
+    const uint64_t prev = __shfl_up(h, 1, 64);
+    const bool head = lane < N && (lane == 0 || h != prev);
+    const unsigned long long hm = __ballot(head);
+    const unsigned long long above = lane < 63 ? (hm & ~((2ull << lane) - 1)) : 0ull;
+    const int next = above ? __builtin_ctzll(above) : N;
+    const int size = head ? next - lane : 0;
+    int maxg = size;
+    UNR for (int m = 32; m > 0; m >>= 1) maxg = max(maxg, __shfl_xor(maxg, m, 64));
+    double acc[9];
+    UNR for (int e = 0; e < 9; e++) acc[e] = c[e];
+    for (int st = 1; st < maxg; st++) {
+        double t[9];
+        UNR for (int e = 0; e < 9; e++) if (e < n) t[e] = __shfl(c[e], (lane + st) & 63, 64);
+        if (head && st < size) UNR for (int e = 0; e < 9; e++) if (e < n) acc[e] = acc[e] + t[e];
+    }
+    const bool keep = head && frob_norm(acc, n) > x.thr;
+    double red[9], ab[9];
+    UNR for (int e = 0; e < 9; e++) {
+        red[e] = (head && !keep && e < n) ? fabs(acc[e]) : 0.0;
+        ab[e] = (keep && e < n) ? fabs(acc[e]) : 0.0;
+    }
+    const unsigned long long km = __ballot(keep);
+    const int K = __popcll(km);
+    const int pos = __popcll(km & ((1ull << lane) - 1));
+    long hoff = 0, coff = 0;
+    int ok = 0;
+    if (lane == 0) {
+        PZH& out = x.H[o];
+        arena_alloc_t0(x, out, K, n);
+        hoff = out.hoff;
+        coff = out.coff;
+        ok = out.cnt == K;
+        x.A->bytes += T.in_bytes() + (double)K * (8.0 + 8.0 * n);
+    }
+    hoff = __shfl(hoff, 0, 64);
+    coff = __shfl(coff, 0, 64);
+    ok = __shfl(ok, 0, 64);
+    if (ok && keep) {
+        x.A->h[hoff + pos] = h;
+        double* dst = x.A->c + coff + (long)pos * n;
+        UNR for (int e = 0; e < 9; e++) if (e < n) dst[e] = acc[e];
+    }
+    UNR for (int e = 0; e < 9; e++) if (e < n) { red[e] = wsum(red[e]); ab[e] = wsum(ab[e]); }
+    if (lane == 0) finish_t0(x.H[o], red, ab, n);
+}
+
+// ---- register bitonic: 256 x E keys, E per thread (element index tid * E + r) -----------------
+template <int E>
+__device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const Terms& T, int N) {
+    const int tid = x.g.tid;
+    uint64_t h[E];
+    uint32_t id[E];
+    UNR for (int r = 0; r < E; r++) {
+        const int idx = tid * E + r;
+        h[r] = idx < N ? T.hash(idx) : ~(uint64_t)0;
+        id[r] = (uint32_t)idx;
+    }
+    const int P = x.g.n * E;
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < E) {
+                UNR for (int r = 0; r < E; r++) {
+                    if ((r & j) == 0) {
+                        const int r2 = r | j;
+                        const bool asc = ((tid * E + r) & k) == 0;
+                        const bool sw = asc ? key_less(h[r2], id[r2], h[r], id[r]) : key_less(h[r], id[r], h[r2], id[r2]);
+                        if (sw) {
+                            const uint64_t th = h[r]; h[r] = h[r2]; h[r2] = th;
+                            const uint32_t ti = id[r]; id[r] = id[r2]; id[r2] = ti;
+                        }
+                    }
+                }
+            } else if (j < 64 * E) {
+                const int m = j / E;
+                UNR for (int r = 0; r < E; r++) {
+                    const uint64_t oh = __shfl_xor(h[r], m, 64);
+                    const uint32_t oi = __shfl_xor(id[r], m, 64);
+                    const int idx = tid * E + r;
+                    const bool asc = (idx & k) == 0, lower = (idx & j) == 0;
+                    const bool other_less = key_less(oh, oi, h[r], id[r]);
+                    if ((lower == asc) ? other_less : !other_less) { h[r] = oh; id[r] = oi; }
+                }
+            } else {
+                UNR for (int r = 0; r < E; r++) { x.kh[tid * E + r] = h[r]; x.ki[tid * E + r] = id[r]; }
+                x.g.sync();
+                UNR for (int r = 0; r < E; r++) {
+                    const int idx = tid * E + r;
+                    const uint64_t oh = x.kh[idx ^ j];
+                    const uint32_t oi = x.ki[idx ^ j];
+                    const bool asc = (idx & k) == 0, lower = (idx & j) == 0;
+                    const bool other_less = key_less(oh, oi, h[r], id[r]);
+                    if ((lower == asc) ? other_less : !other_less) { h[r] = oh; id[r] = oi; }
+                }
+                x.g.sync();
+            }
+        }
+    UNR for (int r = 0; r < E; r++) {
+        const int idx = tid * E + r;
+        if (idx < N) { x.kh[idx] = h[r]; x.ki[idx] = id[r]; }
+    }
+}
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PHASE(k)                                                                                   \
+    if (x.phase && g.tid == 0) {                                                                   \
+        const long long c_ = clock64();                                                            \
+        atomicAdd(&x.phase[k], (unsigned long long)(c_ - ph_t));                                   \
+        ph_t = c_;                                                                                 \
+    }
+#else
+#define PHASE(k)
+#endif
+
+// ---- N > 64: whole group. Header of o set and sources staged (caller's barrier done). ---------
+AI void simplify_big(Ctx& x, int o, const Terms& T, int N) {
     const Grp& g = x.g;
-    const int n = x.H[o].R * x.H[o].C;
+#if defined(__HIP_DEVICE_COMPILE__)
+    long long ph_t = x.phase ? clock64() : 0;
+#endif
+    const int n = T.nout;
     uint64_t* kh = x.kh;
     uint32_t* ki = x.ki;
     int* kp = x.kp;
-    int P = 1;
-    while (P < N) P <<= 1;
-    if (P > x.cap_lds) {
+    const bool in_lds = N <= x.cap_lds;
+    if (!in_lds) {
         kh = x.gkh; ki = x.gki; kp = x.gkp;
+        int P = 1;
+        while (P < N) P <<= 1;
         if (P > x.cap_glb) {
             if (g.tid == 0) { *x.err |= ERR_SORTCAP; x.H[o].cnt = 0; }
-            g.sync();
             return;
         }
     }
-    for (int q = g.tid; q < P; q += g.n) {
-        kh[q] = q < N ? T.hash(q) : ~(uint64_t)0;
-        ki[q] = (uint32_t)q;
+    // order the keys: rank merge of sorted runs, or a sort
+    bool rank_ok = T.runs() <= 6 || (x.mode & 2);
+#if !defined(__HIP_DEVICE_COMPILE__)
+    rank_ok = true;
+#endif
+    if (rank_ok) {
+        for (int p = g.tid; p < N; p += g.n) {
+            const uint64_t h = T.hash(p);
+            const int r = T.rank(p, h);
+            kh[r] = h;
+            ki[r] = (uint32_t)p;
+        }
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+    else if (in_lds) {
+        const int E = N <= 256 ? 1 : N <= 512 ? 2 : N <= 1024 ? 4 : 8;
+        if (E == 1) reg_bitonic<1>(x, T, N);
+        else if (E == 2) reg_bitonic<2>(x, T, N);
+        else if (E == 4) reg_bitonic<4>(x, T, N);
+        else reg_bitonic<8>(x, T, N);
+    }
+#endif
+    else {
+        // many runs and beyond the LDS key capacity: bitonic in global memory
+        int P = 1;
+        while (P < N) P <<= 1;
+        for (int q = g.tid; q < P; q += g.n) {
+            kh[q] = q < N ? T.hash(q) : ~(uint64_t)0;
+            ki[q] = (uint32_t)q;
+        }
+        g.sync();
+        bitonic_mem(x, kh, ki, P);
     }
     g.sync();
-    if (N > 1) bitonic(x, kh, ki, P);
+    PHASE(1)
+    // group sums in term order, keep flags
     double red[9], acc[9], tmp[9];
     UNR for (int e = 0; e < 9; e++) red[e] = 0.0;
     for (int q = g.tid; q < N; q += g.n) {
@@ -285,9 +694,17 @@ ADN void simplify_terms(Ctx& x, int o, const Terms& T, int N) {
         kp[q] = keep;
     }
     g.sync();
+    PHASE(2)
     const int K = block_scan(x, kp, N);
-    alloc_out(x, o, K, n);
+    if (g.tid == 0) {
+        arena_alloc_t0(x, x.H[o], K, n);
+        x.A->bytes += T.in_bytes() + (double)K * (8.0 + 8.0 * n);
+    }
+    g.sync();
+    PHASE(3)
     const long hoff = x.H[o].hoff, coff = x.H[o].coff;
+    double ab[9];
+    UNR for (int e = 0; e < 9; e++) ab[e] = 0.0;
     if (x.H[o].cnt == K) {
         for (int q = g.tid; q < N; q += g.n) {
             const bool head = q == 0 || kh[q] != kh[q - 1];
@@ -302,264 +719,140 @@ ADN void simplify_terms(Ctx& x, int o, const Terms& T, int N) {
             const long pos = kp[q];
             x.A->h[hoff + pos] = kh[q];
             double* dst = x.A->c + coff + pos * n;
-            UNR for (int e = 0; e < 9; e++) if (e < n) dst[e] = acc[e];
+            UNR for (int e = 0; e < 9; e++) if (e < n) { dst[e] = acc[e]; ab[e] = ab[e] + fabs(acc[e]); }
         }
     }
-    block_sum9(x, red);
-    if (g.tid == 0) {
-        if (frob_norm(red, n) != 0)
-            UNR for (int v = 0; v < 2; v++)
-                UNR for (int e = 0; e < 9; e++) if (e < n) x.H[o].ind[v][e] = x.H[o].ind[v][e] + red[e];
-    }
-    g.sync();
+    PHASE(4)
+    double v[18];
+    UNR for (int e = 0; e < 9; e++) { v[e] = red[e]; v[9 + e] = ab[e]; }
+    block_sum(x, v, 18);
+    PHASE(5)
+    if (g.tid == 0) finish_t0(x.H[o], v, v + 9, n);
+}
+
+AI void hdr_init(PZH& h, int R, int C) {
+    h.R = R; h.C = C; h.cnt = 0; h.stride = R * C; h.hoff = 0; h.coff = 0;
+    h.comp = -1; h.scaled = 0; h.scale = 1.0;
+    UNR for (int e = 0; e < 9; e++) { h.center[e] = 0.0; h.ind[0][e] = 0.0; h.ind[1][e] = 0.0; h.absum[e] = 0.0; }
 }
 
 // ---------------------------------------------------------------------------------------------
-// term lists (operands live in LDS handle slots)
-
-// operator* (PZsparse.cu:864-994): T1 a_i x B.c, T2 A.c x b_j, T3 a_i x b_j (hash a_i + b_j)
-struct MulTerms {
-    const Ctx* x;
-    const PZH* A;
-    const PZH* B;
-    AD uint64_t hash(int p) const {
-        const int na = A->cnt, nb = B->cnt;
-        if (p < na) return mono_hash(*x, *A, p);
-        if (p < na + nb) return mono_hash(*x, *B, p - na);
-        const int q = p - na - nb;
-        return mono_hash(*x, *A, q / nb) + mono_hash(*x, *B, q % nb);
-    }
-    AD void prod(const double* a, const double* b, double* out) const {
-        const bool as = A->R == 1 && A->C == 1, bs = B->R == 1 && B->C == 1;
-        if (as) { UNR for (int e = 0; e < 9; e++) out[e] = a[0] * b[e]; }
-        else if (bs) { UNR for (int e = 0; e < 9; e++) out[e] = a[e] * b[0]; }
-        else {
-            matmul(a, A->R, A->C, b, B->C, out);
-            UNR for (int e = 0; e < 9; e++) if (e >= A->R * B->C) out[e] = 0.0;
-        }
-    }
-    AD void coef(int p, double* out) const {
-        const int na = A->cnt, nb = B->cnt;
-        double a[9], b[9];
-        if (p < na) { read_mono(*x, *A, p, a); prod(a, B->center, out); return; }
-        if (p < na + nb) { read_mono(*x, *B, p - na, b); prod(A->center, b, out); return; }
-        const int q = p - na - nb;
-        read_mono(*x, *A, q / nb, a);
-        read_mono(*x, *B, q % nb, b);
-        prod(a, b, out);
-    }
-};
-
-// concatenation of up to 3 sources, each either a full block (place = -1) or a 1x1 source
-// placed at component `place` of the output block (stack / addOneDimPZ)
-struct CatTerms {
-    const Ctx* x;
-    const PZH* S[3];
-    int place[3];
-    AD void which(int p, int& s, int& k) const {
-        s = 0;
-        if (p >= S[0]->cnt) { p -= S[0]->cnt; s = 1; if (p >= S[1]->cnt) { p -= S[1]->cnt; s = 2; } }
-        k = p;
-    }
-    AD uint64_t hash(int p) const { int s, k; which(p, s, k); return mono_hash(*x, *S[s], k); }
-    AD void coef(int p, double* out) const {
-        int s, k;
-        which(p, s, k);
-        read_mono(*x, *S[s], k, out);
-        const int pl = place[s];
-        if (pl >= 0) {
-            const double v = out[0];
-            UNR for (int e = 0; e < 9; e++) out[e] = (e == pl) ? v : 0.0;
-        }
-    }
-};
-
-// ---------------------------------------------------------------------------------------------
-// handle constructors
-
-AD void h_zero(Ctx& x, int o, int R, int C) {
-    if (x.g.tid == 0) hdr_init(x.H[o], R, C);
-    x.g.sync();
-}
-
-// element view (r, c) of handle a  (operator()(r,c), PZsparse.cu:678-697)
-AD void h_elem(Ctx& x, int o, int a, int r, int c) {
-    if (x.g.tid == 0) {
-        const PZH s = x.H[a];
-        PZH& h = x.H[o];
-        h = s;
-        const int e = r + c * s.R;
-        h.R = 1; h.C = 1;
-        h.comp = (s.comp >= 0) ? s.comp : e;
-        h.center[0] = s.center[e];
-        h.ind[0][0] = s.ind[0][e];
-        h.ind[1][0] = s.ind[1][e];
-    }
-    x.g.sync();
-}
-
-// s * a  (PZsparse.cu:996-1030): lazy, no simplify
-AD void h_scale(Ctx& x, int o, double s, int a) {
-    if (x.g.tid == 0) {
-        const PZH src = x.H[a];
-        PZH& h = x.H[o];
-        h = src;
-        const int n = nel(h);
-        for (int e = 0; e < n; e++) {
-            h.center[e] = h.center[e] * s;
-            h.ind[0][e] = h.ind[0][e] * fabs(s);
-            h.ind[1][e] = h.ind[1][e] * fabs(s);
-        }
-        if (src.scaled || src.neg) *x.err |= ERR_HANDLES;  // views never stack scales in this program
-        h.scaled = 1;
-        h.scale = s;
-    }
-    x.g.sync();
-}
-
-// ---------------------------------------------------------------------------------------------
-// operators
+// operators: term list (all threads, uniform) and output header (thread 0: the operator's own
+// centre / independent formula). Operands are never aliased by the output (the program builder
+// allocates SSA-style slots).
 
 // a + b (sign = +1) or a - b (sign = -1)  (PZsparse.cu:743-764, 813-834)
-ADN void op_add(Ctx& x, int o, int a, int b, int sign) {
-    if (x.g.tid == 0) {
-        x.H[x.opa] = x.H[a];
-        x.H[x.opb] = x.H[b];
-        const PZH& A = x.H[x.opa];
-        PZH& B = x.H[x.opb];
-        if (sign < 0) B.neg = !B.neg;
-        PZH& h = x.H[o];
-        hdr_init(h, A.R, A.C);
-        const int n = nel(A);
-        for (int e = 0; e < n; e++) {
+AI void terms_add(const Ctx& x, int a, int b, int sign, Terms& T) {
+    const PZH& A = x.H[a];
+    const PZH& B = x.H[b];
+    T.kind = 1; T.ns = 2;
+    T.S[0] = src_of(x, A); T.S[1] = src_of(x, B);
+    T.places = 0;
+    T.negs = sign < 0 ? 2 : 0;
+    T.nout = nel(A);
+}
+AI void header_add(Ctx& x, int o, int a, int b, int sign) {
+    const PZH& A = x.H[a];
+    const PZH& B = x.H[b];
+    PZH& h = x.H[o];
+    hdr_init(h, A.R, A.C);
+    const int n = nel(A);
+    UNR for (int e = 0; e < 9; e++) {
+        if (e < n) {
             h.center[e] = sign > 0 ? A.center[e] + B.center[e] : A.center[e] - B.center[e];
             h.ind[0][e] = A.ind[0][e] + B.ind[0][e];
             h.ind[1][e] = A.ind[1][e] + B.ind[1][e];
         }
     }
-    x.g.sync();
-    CatTerms T;
-    T.x = &x; T.S[0] = &x.H[x.opa]; T.S[1] = &x.H[x.opb]; T.S[2] = &x.H[x.opb];
-    T.place[0] = -1; T.place[1] = -1; T.place[2] = -1;
-    simplify_terms(x, o, T, x.H[x.opa].cnt + x.H[x.opb].cnt);
 }
 
 // a * b  (PZsparse.cu:864-994)
-ADN void op_mul(Ctx& x, int o, int a, int b) {
-    if (x.g.tid == 0) { x.H[x.opa] = x.H[a]; x.H[x.opb] = x.H[b]; }
-    x.g.sync();
-    const PZH& A = x.H[x.opa];
-    const PZH& B = x.H[x.opb];
-    // |A.c| + sum|a_i| and |B.c| + sum|b_j| for the independent part, reduced over the group
-    double sa[9], sb[9], m[9];
-    UNR for (int e = 0; e < 9; e++) { sa[e] = 0.0; sb[e] = 0.0; }
-    for (int k = x.g.tid; k < A.cnt; k += x.g.n) { read_mono(x, A, k, m); UNR for (int e = 0; e < 9; e++) sa[e] = sa[e] + fabs(m[e]); }
-    block_sum9(x, sa);
-    for (int k = x.g.tid; k < B.cnt; k += x.g.n) { read_mono(x, B, k, m); UNR for (int e = 0; e < 9; e++) sb[e] = sb[e] + fabs(m[e]); }
-    block_sum9(x, sb);
-    MulTerms T;
-    T.x = &x; T.A = &A; T.B = &B;
-    if (x.g.tid == 0) {
-        const bool as = A.R == 1 && A.C == 1, bs = B.R == 1 && B.C == 1;
-        PZH& h = x.H[o];
-        hdr_init(h, as ? B.R : A.R, as ? B.C : (bs ? A.C : B.C));
-        const int na = nel(A), nb = nel(B), nr = nel(h);
-        double cen[9];
-        T.prod(A.center, B.center, cen);
-        for (int e = 0; e < nr; e++) h.center[e] = cen[e];
-        double r2[9], r3[9];
-        for (int e = 0; e < 9; e++) { r2[e] = 0.0; r3[e] = 0.0; }
-        for (int e = 0; e < na; e++) r2[e] = fabs(A.center[e]) + sa[e];
-        for (int e = 0; e < nb; e++) r3[e] = fabs(B.center[e]) + sb[e];
-        for (int v = 0; v < 2; v++) {
-            double t2[9], t3[9], ii[9];
-            if (as) { for (int e = 0; e < nb; e++) t2[e] = r2[0] * B.ind[v][e]; }
-            else if (bs) { for (int e = 0; e < na; e++) t2[e] = r2[e] * B.ind[v][0]; }
-            else matmul(r2, A.R, A.C, B.ind[v], B.C, t2);
-            if (as) { for (int e = 0; e < nb; e++) t3[e] = A.ind[v][0] * r3[e]; }
-            else if (bs) { for (int e = 0; e < na; e++) t3[e] = A.ind[v][e] * r3[0]; }
-            else matmul(A.ind[v], A.R, A.C, r3, B.C, t3);
-            if (as) { for (int e = 0; e < nr; e++) ii[e] = A.ind[v][0] * B.ind[v][e]; }
-            else if (bs) { for (int e = 0; e < nr; e++) ii[e] = A.ind[v][e] * B.ind[v][0]; }
-            else matmul(A.ind[v], A.R, A.C, B.ind[v], B.C, ii);
-            for (int e = 0; e < nr; e++) h.ind[v][e] = ii[e] + (t2[e] + t3[e]);
-        }
-        if (as && !bs && B.R != 1 && A.cnt > 0 && B.cnt > 0) *x.err |= ERR_HANDLES;  // Eigen assert in the reference
+AI void terms_mul(const Ctx& x, int a, int b, Terms& T) {
+    const PZH& A = x.H[a];
+    const PZH& B = x.H[b];
+    T.kind = 0; T.ns = 2;
+    T.places = 0; T.negs = 0;
+    T.S[0] = src_of(x, A); T.S[1] = src_of(x, B);
+    T.Ac = A.center; T.Bc = B.center;
+    T.AR = A.R; T.AC = A.C; T.BC = B.C;
+    const bool as = A.R == 1 && A.C == 1, bs = B.R == 1 && B.C == 1;
+    T.nout = as ? nel(B) : (bs ? nel(A) : A.R * B.C);
+}
+// centre, then the dual independent part
+//   ind = A.ind B.ind + (|A.c| + sum|a_i|) B.ind + A.ind (|B.c| + sum|b_j|)
+AI void header_mul(Ctx& x, int o, int a, int b, const Terms& T) {
+    const PZH& A = x.H[a];
+    const PZH& B = x.H[b];
+    const bool as = A.R == 1 && A.C == 1, bs = B.R == 1 && B.C == 1;
+    PZH& h = x.H[o];
+    hdr_init(h, as ? B.R : A.R, as ? B.C : (bs ? A.C : B.C));
+    const int na = nel(A), nb = nel(B), nr = nel(h);
+    double cen[9], ac[9], bc[9], r2[9], r3[9];
+    UNR for (int e = 0; e < 9; e++) {
+        ac[e] = A.center[e];
+        bc[e] = B.center[e];
+        r2[e] = e < na ? fabs(A.center[e]) + A.absum[e] : 0.0;
+        r3[e] = e < nb ? fabs(B.center[e]) + B.absum[e] : 0.0;
     }
-    x.g.sync();
-    simplify_terms(x, o, T, A.cnt + B.cnt + A.cnt * B.cnt);
+    T.prod(ac, bc, cen);
+    UNR for (int e = 0; e < 9; e++) if (e < nr) h.center[e] = cen[e];
+    UNR for (int v = 0; v < 2; v++) {
+        double ai[9], bi[9], t2[9], t3[9], ii[9];
+        UNR for (int e = 0; e < 9; e++) { ai[e] = A.ind[v][e]; bi[e] = B.ind[v][e]; }
+        if (as) {
+            UNR for (int e = 0; e < 9; e++) { t2[e] = r2[0] * bi[e]; t3[e] = ai[0] * r3[e]; ii[e] = ai[0] * bi[e]; }
+        } else if (bs) {
+            UNR for (int e = 0; e < 9; e++) { t2[e] = r2[e] * bi[0]; t3[e] = ai[e] * r3[0]; ii[e] = ai[e] * bi[0]; }
+        } else {
+            matmul(r2, A.R, A.C, bi, B.C, t2);
+            matmul(ai, A.R, A.C, r3, B.C, t3);
+            matmul(ai, A.R, A.C, bi, B.C, ii);
+        }
+        UNR for (int e = 0; e < 9; e++) if (e < nr) h.ind[v][e] = ii[e] + (t2[e] + t3[e]);
+    }
+    if (as && !bs && B.R != 1 && A.cnt > 0 && B.cnt > 0) *x.err |= ERR_HANDLES;  // Eigen assert in the reference
+    if (!as && !bs && !(A.R == 3 && A.C == 3 && B.R == 3)) *x.err |= ERR_HANDLES;  // block shape outside matmul()
 }
 
 // stack three 1x1 PZs into a 3x1 (PZsparse.cu:1087-1116)
-ADN void op_stack3(Ctx& x, int o, int a0, int a1, int a2) {
-    if (x.g.tid == 0) {
-        x.H[x.opa] = x.H[a0];
-        x.H[x.opb] = x.H[a1];
-        x.H[x.opc] = x.H[a2];
-        PZH& h = x.H[o];
-        hdr_init(h, 3, 1);
-        const PZH* S[3] = {&x.H[x.opa], &x.H[x.opb], &x.H[x.opc]};
-        for (int i = 0; i < 3; i++) { h.center[i] = S[i]->center[0]; h.ind[0][i] = S[i]->ind[0][0]; h.ind[1][i] = S[i]->ind[1][0]; }
+AI void terms_stack3(const Ctx& x, int a0, int a1, int a2, Terms& T) {
+    T.kind = 1; T.ns = 3;
+    T.S[0] = src_of(x, x.H[a0]); T.S[1] = src_of(x, x.H[a1]); T.S[2] = src_of(x, x.H[a2]);
+    T.places = 1 | (2 << 4) | (3 << 8);
+    T.negs = 0;
+    T.nout = 3;
+}
+AI void header_stack3(Ctx& x, int o, int a0, int a1, int a2) {
+    const PZH& S0 = x.H[a0];
+    const PZH& S1 = x.H[a1];
+    const PZH& S2 = x.H[a2];
+    PZH& h = x.H[o];
+    hdr_init(h, 3, 1);
+    h.center[0] = S0.center[0]; h.ind[0][0] = S0.ind[0][0]; h.ind[1][0] = S0.ind[1][0];
+    h.center[1] = S1.center[0]; h.ind[0][1] = S1.ind[0][0]; h.ind[1][1] = S1.ind[1][0];
+    h.center[2] = S2.center[0]; h.ind[0][2] = S2.ind[0][0]; h.ind[1][2] = S2.ind[1][0];
+}
+
+// self(e) += a (1x1)  (PZsparse.cu:1068-1085)
+AI void terms_add_one_dim(const Ctx& x, int self, int a, int e, Terms& T) {
+    const PZH& A = x.H[self];
+    T.kind = 1; T.ns = 2;
+    T.S[0] = src_of(x, A); T.S[1] = src_of(x, x.H[a]);
+    T.places = (e + 1) << 4;
+    T.negs = 0;
+    T.nout = nel(A);
+}
+AI void header_add_one_dim(Ctx& x, int o, int self, int a, int e) {
+    const PZH& A = x.H[self];
+    const PZH& B = x.H[a];
+    PZH& h = x.H[o];
+    hdr_init(h, A.R, A.C);
+    UNR for (int q = 0; q < 9; q++) {
+        const bool at = q == e;
+        h.center[q] = at ? A.center[q] + B.center[0] : A.center[q];
+        h.ind[0][q] = at ? A.ind[0][q] + B.ind[0][0] : A.ind[0][q];
+        h.ind[1][q] = at ? A.ind[1][q] + B.ind[1][0] : A.ind[1][q];
     }
-    x.g.sync();
-    CatTerms T;
-    T.x = &x; T.S[0] = &x.H[x.opa]; T.S[1] = &x.H[x.opb]; T.S[2] = &x.H[x.opc];
-    T.place[0] = 0; T.place[1] = 1; T.place[2] = 2;
-    simplify_terms(x, o, T, x.H[x.opa].cnt + x.H[x.opb].cnt + x.H[x.opc].cnt);
-}
-
-// self(r,c) += a (1x1)  (PZsparse.cu:1068-1085); result written to o
-ADN void op_add_one_dim(Ctx& x, int o, int self, int a, int r, int c) {
-    const int e = r + c * 3;
-    if (x.g.tid == 0) {
-        x.H[x.opa] = x.H[self];
-        x.H[x.opb] = x.H[a];
-        const PZH& A = x.H[x.opa];
-        const PZH& B = x.H[x.opb];
-        PZH& h = x.H[o];
-        hdr_init(h, A.R, A.C);
-        for (int q = 0; q < 9; q++) { h.center[q] = A.center[q]; h.ind[0][q] = A.ind[0][q]; h.ind[1][q] = A.ind[1][q]; }
-        h.center[e] += B.center[0];
-        h.ind[0][e] += B.ind[0][0];
-        h.ind[1][e] += B.ind[1][0];
-    }
-    x.g.sync();
-    CatTerms T;
-    T.x = &x; T.S[0] = &x.H[x.opa]; T.S[1] = &x.H[x.opb]; T.S[2] = &x.H[x.opb];
-    T.place[0] = -1; T.place[1] = e; T.place[2] = -1;
-    simplify_terms(x, o, T, x.H[x.opa].cnt + x.H[x.opb].cnt);
-}
-
-// cross products (PZsparse.cu:1118-1167); handles t0 .. t0+10 are scratch slots
-ADN void op_cross_mp(Ctx& x, int o, const double* a, int b, int t0) {
-    const int e0 = t0, e1 = t0 + 1, e2 = t0 + 2, s0 = t0 + 3, s1 = t0 + 4, r0 = t0 + 5, r1 = t0 + 6, r2 = t0 + 7;
-    const double a0 = a[0], a1 = a[1], a2 = a[2];
-    h_elem(x, e0, b, 0, 0); h_elem(x, e1, b, 1, 0); h_elem(x, e2, b, 2, 0);
-    h_scale(x, s0, a1, e2); h_scale(x, s1, a2, e1); op_add(x, r0, s0, s1, -1);
-    h_scale(x, s0, a2, e0); h_scale(x, s1, a0, e2); op_add(x, r1, s0, s1, -1);
-    h_scale(x, s0, a0, e1); h_scale(x, s1, a1, e0); op_add(x, r2, s0, s1, -1);
-    op_stack3(x, o, r0, r1, r2);
-}
-
-ADN void op_cross_pm(Ctx& x, int o, int a, const double* b, int t0) {
-    const int e0 = t0, e1 = t0 + 1, e2 = t0 + 2, s0 = t0 + 3, s1 = t0 + 4, r0 = t0 + 5, r1 = t0 + 6, r2 = t0 + 7;
-    const double b0 = b[0], b1 = b[1], b2 = b[2];
-    h_elem(x, e0, a, 0, 0); h_elem(x, e1, a, 1, 0); h_elem(x, e2, a, 2, 0);
-    h_scale(x, s0, b2, e1); h_scale(x, s1, b1, e2); op_add(x, r0, s0, s1, -1);
-    h_scale(x, s0, b0, e2); h_scale(x, s1, b2, e0); op_add(x, r1, s0, s1, -1);
-    h_scale(x, s0, b1, e0); h_scale(x, s1, b0, e1); op_add(x, r2, s0, s1, -1);
-    op_stack3(x, o, r0, r1, r2);
-}
-
-ADN void op_cross_pp(Ctx& x, int o, int a, int b, int t0) {
-    const int a0 = t0, a1 = t0 + 1, a2 = t0 + 2, b0 = t0 + 3, b1 = t0 + 4, b2 = t0 + 5;
-    const int p = t0 + 6, q = t0 + 7, r0 = t0 + 8, r1 = t0 + 9, r2 = t0 + 10;
-    h_elem(x, a0, a, 0, 0); h_elem(x, a1, a, 1, 0); h_elem(x, a2, a, 2, 0);
-    h_elem(x, b0, b, 0, 0); h_elem(x, b1, b, 1, 0); h_elem(x, b2, b, 2, 0);
-    op_mul(x, p, a1, b2); op_mul(x, q, a2, b1); op_add(x, r0, p, q, -1);
-    op_mul(x, p, a2, b0); op_mul(x, q, a0, b2); op_add(x, r1, p, q, -1);
-    op_mul(x, p, a0, b1); op_mul(x, q, a1, b0); op_add(x, r2, p, q, -1);
-    op_stack3(x, o, r0, r1, r2);
 }
 
 }  // namespace armour

@@ -4,6 +4,8 @@
 // KPR/armour_main.cu:118-211; runs as one 256-thread workgroup on gfx950 (reach_kernel in
 // reach_kernel.hip) or sequentially in the CPU emulation used by tests.
 #pragma once
+#include <initializer_list>
+#include <vector>
 #include "interval.h"
 #include "pz_engine.h"
 
@@ -83,7 +85,7 @@ AD void bound_k_indep(double vlb, double vub, double s_lb, double s_ub, double e
 }
 
 // KPR/Trajectory.cu:63-245 for joint i over [s_ind/T, (s_ind+1)/T]
-ADN JrsJoint jrs_joint(const RobotParams& rp, int T, int s_ind, int i, double q0, double qd0, double qdd0) {
+__host__ __device__ __attribute__((noinline)) JrsJoint jrs_joint(const RobotParams& rp, int T, int s_ind, int i, double q0, double qd0, double qdd0) {
     const double D = rp.duration;
     const double Tqd0 = qd0 * D, TTqdd0 = qdd0 * D * D;
     const double ds = 1.0 / T;
@@ -163,365 +165,616 @@ ADN JrsJoint jrs_joint(const RobotParams& rp, int T, int s_ind, int i, double q0
     return J;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The reach program. The op sequence of one job depends only on the robot (joint axes, NJ), so
+// the host builds it once (ProgramBuilder) as a tape of Ops with SSA-style handle slots (an
+// output never aliases an operand, so operands are read in place — no staging copies), and the
+// kernel interprets it: one switch whose bodies are force-inlined, one barrier per op.
+
+enum : int {
+    OP_JRS, OP_MAKE1D, OP_MAKEROT, OP_MAKEBOX, OP_CONST, OP_ZERO, OP_VIEW, OP_TRANSPOSE,
+    OP_MUL, OP_ADD, OP_STACK3, OP_ADD1D, OP_EMIT_LINK, OP_EMIT_TORQUE, OP_TORQUE_RADIUS, OP_NCODES
+};
+enum : int { CONST_RPY = 0, CONST_TRANS = 1, CONST_MASS = 2, CONST_INERTIA = 3 };
+
+struct Op {
+    int code;
+    int o, a, b, c;
+    int i;
+    int sync;   // barrier after this op
+    int pad;
+    double s;
+};
+
+constexpr int MAX_SLOTS = 72;
+
+// thread-0 bodies are inlined too: an out-of-line variant (stack arrays passed through a lambda
+// into a nested out-of-line call) was miscompiled for gfx950 — tools/dump_ops.py localised it to
+// MAKEROT writing the wrong centre element
+#define T0FN __host__ __device__ inline __attribute__((always_inline))
+
+// ---- thread-0 bodies ----------------------------------------------------------------------
+
 // PZ from raw candidate monomials with the reference constructor's simplify (PZsparse.cu:120-205)
-// — tiny lists, done by thread 0
-ADN void h_make_raw(Ctx& x, int o, int R, int C, const double* center, int nc, const uint64_t* hs, const double (*cf)[9]) {
-    if (x.g.tid == 0) {
-        const int n = R * C;
-        int ord[4];
-        for (int i = 0; i < nc; i++) ord[i] = i;
-        for (int i = 1; i < nc; i++)  // insertion sort by hash (stable, as std::sort for n <= 16)
-            for (int j = i; j > 0 && hs[ord[j]] < hs[ord[j - 1]]; j--) { const int t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
-        double keep_c[4][9];
-        uint64_t keep_h[4];
-        int K = 0;
-        double red[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        int i = 0;
-        while (i < nc) {
-            double acc[9];
-            for (int e = 0; e < n; e++) acc[e] = cf[ord[i]][e];
-            int j = i + 1;
-            for (; j < nc && hs[ord[j]] == hs[ord[i]]; j++)
-                for (int e = 0; e < n; e++) acc[e] = acc[e] + cf[ord[j]][e];
-            if (frob_norm(acc, n) <= x.thr) {
-                for (int e = 0; e < n; e++) red[e] = red[e] + fabs(acc[e]);
-            } else {
-                for (int e = 0; e < n; e++) keep_c[K][e] = acc[e];
-                keep_h[K] = hs[ord[i]];
-                K++;
-            }
-            i = j;
-        }
-        PZH& h = x.H[o];
-        h.R = R; h.C = C; h.comp = -1; h.scaled = 0; h.neg = 0; h.scale = 1.0; h.stride = n;
-        for (int e = 0; e < 9; e++) { h.center[e] = e < n ? center[e] : 0.0; h.ind[0][e] = 0.0; h.ind[1][e] = 0.0; }
-        if (frob_norm(red, n) != 0)
-            for (int e = 0; e < n; e++) { h.ind[0][e] += red[e]; h.ind[1][e] += red[e]; }
-        if (x.A->hused + K > x.A->hcap || x.A->cused + (long)K * n > x.A->ccap) {
-            *x.err |= ERR_ARENA;
-            h.cnt = 0; h.hoff = 0; h.coff = 0;
+T0FN void t0_make_raw(Ctx& x, int o, int R, int C, const double* center, int nc, const uint64_t* hs, const double (*cf)[9]) {
+    const int n = R * C;
+    int ord[4];
+    for (int i = 0; i < nc; i++) ord[i] = i;
+    for (int i = 1; i < nc; i++)  // insertion sort by hash (stable)
+        for (int j = i; j > 0 && hs[ord[j]] < hs[ord[j - 1]]; j--) { const int t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
+    double keep_c[4][9];
+    uint64_t keep_h[4];
+    int K = 0;
+    double red[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int i = 0;
+    while (i < nc) {
+        double acc[9];
+        for (int e = 0; e < 9; e++) acc[e] = e < n ? cf[ord[i]][e] : 0.0;
+        int j = i + 1;
+        for (; j < nc && hs[ord[j]] == hs[ord[i]]; j++)
+            for (int e = 0; e < n; e++) acc[e] = acc[e] + cf[ord[j]][e];
+        if (frob_norm(acc, n) <= x.thr) {
+            for (int e = 0; e < n; e++) red[e] = red[e] + fabs(acc[e]);
         } else {
-            h.cnt = K; h.hoff = x.A->hused; h.coff = x.A->cused;
-            for (int k = 0; k < K; k++) {
-                x.A->h[h.hoff + k] = keep_h[k];
-                for (int e = 0; e < n; e++) x.A->c[h.coff + (long)k * n + e] = keep_c[k][e];
-            }
-            x.A->hused += K;
-            x.A->cused += (long)K * n;
+            for (int e = 0; e < 9; e++) keep_c[K][e] = acc[e];
+            keep_h[K] = hs[ord[i]];
+            K++;
         }
+        i = j;
     }
-    x.g.sync();
+    PZH& h = x.H[o];
+    hdr_init(h, R, C);
+    for (int e = 0; e < n; e++) h.center[e] = center[e];
+    if (frob_norm(red, n) != 0)
+        for (int e = 0; e < n; e++) { h.ind[0][e] += red[e]; h.ind[1][e] += red[e]; }
+    for (int k = 0; k < K; k++)
+        for (int e = 0; e < n; e++) h.absum[e] += fabs(keep_c[k][e]);
+    arena_alloc_t0(x, h, K, n);
+    if (h.cnt == K)
+        for (int k = 0; k < K; k++) {
+            x.A->h[h.hoff + k] = keep_h[k];
+            for (int e = 0; e < n; e++) x.A->c[h.coff + (long)k * n + e] = keep_c[k][e];
+        }
 }
 
-// constant PZ (no monomials): PZsparse(const MatrixXd&, double uncertainty) (PZsparse.cu:75-98)
-AD void h_const(Ctx& x, int o, int R, int C, const double* center, double unc_int) {
-    if (x.g.tid == 0) {
-        PZH& h = x.H[o];
-        const int n = R * C;
-        h.R = R; h.C = C; h.cnt = 0; h.hoff = 0; h.coff = 0; h.stride = n; h.comp = -1; h.scaled = 0; h.neg = 0; h.scale = 1.0;
-        for (int e = 0; e < 9; e++) {
-            h.center[e] = e < n ? center[e] : 0.0;
-            h.ind[0][e] = 0.0;
-            h.ind[1][e] = e < n ? unc_int * fabs(center[e]) : 0.0;
-        }
+// constant PZ (no monomials): PZsparse(const MatrixXd&, double uncertainty) (PZsparse.cu:75-98);
+// the uncertainty enters only the interval part (ind[1]) of the fused nominal/interval pair
+T0FN void t0_const(Ctx& x, int o, int R, int C, const double* center, double unc_int) {
+    PZH& h = x.H[o];
+    hdr_init(h, R, C);
+    const int n = R * C;
+    for (int e = 0; e < n; e++) {
+        h.center[e] = center[e];
+        h.ind[1][e] = unc_int * fabs(center[e]);
     }
-    x.g.sync();
 }
 
-// materialised transpose of a full handle (PZsparse.cu:1050-1066)
-ADN void op_transpose(Ctx& x, int o, int a) {
-    if (x.g.tid == 0) {
-        x.H[x.opa] = x.H[a];
-        const PZH& A = x.H[x.opa];
-        PZH& h = x.H[o];
-        hdr_init(h, A.C, A.R);
-        for (int i = 0; i < A.R; i++)
-            for (int j = 0; j < A.C; j++) {
-                h.center[j + i * A.C] = A.center[i + j * A.R];
-                h.ind[0][j + i * A.C] = A.ind[0][i + j * A.R];
-                h.ind[1][j + i * A.C] = A.ind[1][i + j * A.R];
-            }
+// element (e >= 0) and/or scale view of a full handle: operator()(r,c) (PZsparse.cu:678-697)
+// and PZ * double (PZsparse.cu:996-1030) — lazy, no simplify
+T0FN void t0_view(Ctx& x, int o, int a, int e, int scaled, double s) {
+    const PZH& P = x.H[a];
+    PZH& h = x.H[o];
+    const int n = e >= 0 ? 1 : nel(P);
+    h.R = e >= 0 ? 1 : P.R;
+    h.C = e >= 0 ? 1 : P.C;
+    h.cnt = P.cnt; h.stride = P.stride; h.hoff = P.hoff; h.coff = P.coff;
+    h.comp = e >= 0 ? e : P.comp;
+    h.scaled = scaled;
+    h.scale = scaled ? s : 1.0;
+    if (P.comp >= 0 || P.scaled) *x.err |= ERR_HANDLES;  // views of views never occur in this program
+    for (int q = 0; q < 9; q++) {
+        const int src = e >= 0 ? e : q;
+        double c = 0.0, i0 = 0.0, i1 = 0.0;
+        if (q < n) { c = P.center[src]; i0 = P.ind[0][src]; i1 = P.ind[1][src]; }
+        double ab = q < n ? P.absum[src] : 0.0;
+        if (scaled) { c = c * s; i0 = i0 * fabs(s); i1 = i1 * fabs(s); ab = ab * fabs(s); }
+        h.center[q] = c; h.ind[0][q] = i0; h.ind[1][q] = i1; h.absum[q] = ab;
     }
-    x.g.sync();
-    const PZH& A = x.H[x.opa];
+}
+
+// materialised transpose of a full handle (PZsparse.cu:1050-1066); operands are rotations with
+// a handful of monomials, so thread 0 copies them
+T0FN void t0_transpose(Ctx& x, int o, int a) {
+    const PZH& A = x.H[a];
+    PZH& h = x.H[o];
+    hdr_init(h, A.C, A.R);
+    for (int i = 0; i < A.R; i++)
+        for (int j = 0; j < A.C; j++) {
+            h.center[j + i * A.C] = A.center[i + j * A.R];
+            h.ind[0][j + i * A.C] = A.ind[0][i + j * A.R];
+            h.ind[1][j + i * A.C] = A.ind[1][i + j * A.R];
+            h.absum[j + i * A.C] = A.absum[i + j * A.R];
+        }
     const int n = nel(A);
-    alloc_out(x, o, A.cnt, n);
-    const PZH& O = x.H[o];
-    if (O.cnt == A.cnt)
-        for (int k = x.g.tid; k < A.cnt; k += x.g.n) {
+    arena_alloc_t0(x, h, A.cnt, n);
+    if (h.cnt == A.cnt)
+        for (int k = 0; k < A.cnt; k++) {
             double m[9];
             read_mono(x, A, k, m);
-            x.A->h[O.hoff + k] = mono_hash(x, A, k);
+            x.A->h[h.hoff + k] = mono_hash(x, A, k);
             for (int i = 0; i < A.R; i++)
-                for (int j = 0; j < A.C; j++) x.A->c[O.coff + (long)k * n + j + i * A.C] = m[i + j * A.R];
+                for (int jj = 0; jj < A.C; jj++) x.A->c[h.coff + (long)k * n + jj + i * A.C] = m[i + jj * A.R];
         }
-    x.g.sync();
+    x.A->bytes += 2.0 * A.cnt * (8.0 + 8.0 * n);
 }
 
-// handle slots
-namespace hs {
-constexpr int R0 = 0;                       // R[0..MAX_J]       (MAX_J + 1)
-constexpr int RT0 = R0 + MAX_J + 1;         // R_t[0..MAX_J-1]
-constexpr int QD0 = RT0 + MAX_J;            // qd_des[0..NF-1]
-constexpr int QDA0 = QD0 + NF;              // qda_des
-constexpr int QDD0 = QDA0 + NF;             // qdda_des
-constexpr int F0 = QDD0 + NF;               // F[0..MAX_J-1]
-constexpr int N0 = F0 + MAX_J;              // N[0..MAX_J-1]
-constexpr int W = N0 + MAX_J, WDOT = W + 1, WAUX = W + 2, LIN = W + 3, FF = W + 4, NN = W + 5;
-constexpr int T1 = W + 6, T2 = T1 + 1, T3 = T1 + 2, T4 = T1 + 3, T5 = T1 + 4, T6 = T1 + 5, T7 = T1 + 6;
-constexpr int CA = T1 + 8;                  // cross scratch A (11 slots)
-constexpr int CB = CA + 11;                 // cross scratch B (11 slots)
-constexpr int OPA = CB + 11, OPB = OPA + 1, OPC = OPA + 2;  // operand staging
-constexpr int COUNT = OPA + 3;
-}  // namespace hs
+T0FN void t0_make_1d(Ctx& x, int o, const JrsJoint& J, int i, int v) {
+    // qd / qda / qdda 1-D PZs: k_i and qde_i / qdae_i / qddae_i monomials (Trajectory.cu:151-244)
+    const double c0 = v == 2 ? J.qdd_c : J.qd_c;
+    uint64_t hh[2];
+    double cf[2][9];
+    hh[0] = slot_hash(SLOT_K + i);
+    cf[0][0] = v == 2 ? J.qdd_k : J.qd_k;
+    hh[1] = slot_hash((v == 0 ? SLOT_QDE : v == 1 ? SLOT_QDAE : SLOT_QDDAE) + i);
+    cf[1][0] = v == 0 ? J.qd_e : v == 1 ? J.qda_e : J.qdd_e;
+    t0_make_raw(x, o, 1, 1, &c0, 2, hh, cf);
+}
 
-// outputs of one link / torque PZ
-ADN void emit_link(Ctx& x, const ReachOut& out, long j, int l) {
-    // reduce_link_PZ (PZsparse.cu:370-402) in monomial order, then emit the k-only part
-    const int L = l;
-    if (x.g.tid == 0) {
-        PZH& h = x.H[hs::T7];
-        const long base = (j * out.NJ + L);
-        double* gens = out.link_gens + base * 18;
-        for (int e = 0; e < 18; e++) gens[e] = 0.0;
-        int jg = 0, kk = 0;
-        double ind[3] = {h.ind[0][0], h.ind[0][1], h.ind[0][2]};
-        for (int k = 0; k < h.cnt; k++) {
-            const uint64_t hh = x.A->h[h.hoff + k];
-            const double* c = x.A->c + h.coff + (long)k * 3;
-            if (hh < HASH_K_ONLY) {
-                if (kk < CAP_LM) {
-                    out.link_hash[base * CAP_LM + kk] = (uint16_t)hh;
-                    for (int e = 0; e < 3; e++) out.link_coef[(base * CAP_LM + kk) * 3 + e] = c[e];
-                } else {
-                    *x.err |= ERR_OUTCAP;
-                }
-                kk++;
-            } else if (hh < HASH_K_LINKS_ONLY && (hh & K_MASK) == 0) {
-                if (jg < 3) { for (int e = 0; e < 3; e++) gens[e + 3 * jg] = c[e]; }
-                else *x.err |= ERR_LINKGEN;
-                jg++;
-            } else {
-                for (int e = 0; e < 3; e++) ind[e] += fabs(c[e]);
-            }
-        }
-        gens[0 + 3 * 3] = ind[0];
-        gens[1 + 3 * 4] = ind[1];
-        gens[2 + 3 * 5] = ind[2];
-        out.link_cnt[base] = kk < CAP_LM ? kk : CAP_LM;
-        for (int e = 0; e < 3; e++) { out.link_center[base * 3 + e] = h.center[e]; out.link_rad[base * 3 + e] = ind[e]; }
+T0FN void t0_make_rot(Ctx& x, int o, const RobotParams& rp, const JrsJoint& J, int i) {
+    // rotation PZ about the joint axis (PZsparse.cu:179-205 + makeRotationMatrix :211-250)
+    const int ax = rp.axes[i];
+    double cen[9], cf[4][9];
+    uint64_t hh[4];
+    for (int e = 0; e < 9; e++) cen[e] = (e % 4 == 0) ? 1.0 : 0.0;
+    for (int m = 0; m < 4; m++) for (int e = 0; e < 9; e++) cf[m][e] = 0.0;
+    auto put = [&](double* Rm, double c, double s) {
+        const double ns = -1.0 * s;
+        if (ax == 1) { Rm[1 + 3] = c; Rm[1 + 6] = ns; Rm[2 + 3] = s; Rm[2 + 6] = c; }
+        else if (ax == 2) { Rm[0] = c; Rm[0 + 6] = s; Rm[2] = ns; Rm[2 + 6] = c; }
+        else { Rm[0] = c; Rm[0 + 3] = ns; Rm[1] = s; Rm[1 + 3] = c; }
+    };
+    put(cen, J.cos_c, J.sin_c);
+    put(cf[0], J.cos_k, 0.0); hh[0] = slot_hash(SLOT_K + i);
+    put(cf[1], J.cos_e, 0.0); hh[1] = slot_hash(SLOT_COS + i);
+    put(cf[2], 0.0, J.sin_k); hh[2] = slot_hash(SLOT_K + i);
+    put(cf[3], 0.0, J.sin_e); hh[3] = slot_hash(SLOT_SIN + i);
+    t0_make_raw(x, o, 3, 3, cen, 4, hh, cf);
+}
+
+T0FN void t0_make_box(Ctx& x, int o, const RobotParams& rp, int i) {
+    // link box: generators on the qde_0 / qdae_0 / qddae_0 slots (Dynamics.cu:98-116)
+    uint64_t hh[3];
+    double cf[3][9];
+    for (int m = 0; m < 3; m++) {
+        for (int e = 0; e < 9; e++) cf[m][e] = 0.0;
+        cf[m][m] = rp.link_g[i][m];
+        hh[m] = slot_hash(NF * (m + 1));
     }
-    x.g.sync();
+    t0_make_raw(x, o, 3, 1, rp.link_c[i], 3, hh, cf);
 }
 
-ADN void emit_torque(Ctx& x, const ReachOut& out, long j, int i, double* rdist, double* ured) {
-    if (x.g.tid == 0) {
-        PZH& h = x.H[hs::T7];
-        const long base = j * NF + i;
-        // disturbance u_int - u_nom: centres and monomials cancel exactly, the independent parts
-        // add (armour_main.cu:135-137, PZsparse.cu:813-834)
-        rdist[i] = h.ind[1][0] + h.ind[0][0];
-        // reduce (PZsparse.cu:352-368)
-        double ind = h.ind[0][0];
-        int kk = 0;
-        for (int k = 0; k < h.cnt; k++) {
-            const uint64_t hh = x.A->h[h.hoff + k];
-            double c = x.A->c[h.coff + (long)k * h.stride + (h.comp >= 0 ? h.comp : 0)];
-            if (h.scaled) c = h.scale * c;
-            if (h.neg) c = -c;
-            if (hh < HASH_K_ONLY) {
-                if (kk < CAP_UM) {
-                    out.tq_hash[base * CAP_UM + kk] = (uint16_t)hh;
-                    out.tq_coef[base * CAP_UM + kk] = c;
-                } else {
-                    *x.err |= ERR_OUTCAP;
-                }
-                kk++;
+// reduce_link_PZ (PZsparse.cu:370-402) in monomial order, then emit the k-only part
+T0FN void t0_emit_link(Ctx& x, const ReachOut& out, long j, int a, int l) {
+    const PZH& h = x.H[a];
+    const long base = j * out.NJ + l;
+    double* gens = out.link_gens + base * 18;
+    double gl[18];
+    for (int e = 0; e < 18; e++) gl[e] = 0.0;
+    int jg = 0, kk = 0;
+    double ind[3] = {h.ind[0][0], h.ind[0][1], h.ind[0][2]};
+    for (int k = 0; k < h.cnt; k++) {
+        const uint64_t hh = x.A->h[h.hoff + k];
+        const double* c = x.A->c + h.coff + (long)k * 3;
+        if (hh < HASH_K_ONLY) {
+            if (kk < CAP_LM) {
+                out.link_hash[base * CAP_LM + kk] = (uint16_t)hh;
+                for (int e = 0; e < 3; e++) out.link_coef[(base * CAP_LM + kk) * 3 + e] = c[e];
             } else {
-                ind += fabs(c);
+                *x.err |= ERR_OUTCAP;
             }
+            kk++;
+        } else if (hh < HASH_K_LINKS_ONLY && (hh & K_MASK) == 0) {
+            if (jg < 3) { for (int e = 0; e < 3; e++) gl[e + 3 * jg] = c[e]; }
+            else *x.err |= ERR_LINKGEN;
+            jg++;
+        } else {
+            for (int e = 0; e < 3; e++) ind[e] += fabs(c[e]);
         }
-        out.tq_cnt[base] = kk < CAP_UM ? kk : CAP_UM;
-        out.tq_center[base] = h.center[0];
-        out.tq_rad[base] = ind;
-        ured[i] = ind;
     }
-    x.g.sync();
+    gl[0 + 3 * 3] = ind[0];
+    gl[1 + 3 * 4] = ind[1];
+    gl[2 + 3 * 5] = ind[2];
+    for (int e = 0; e < 18; e++) gens[e] = gl[e];
+    out.link_cnt[base] = kk < CAP_LM ? kk : CAP_LM;
+    for (int e = 0; e < 3; e++) { out.link_center[base * 3 + e] = h.center[e]; out.link_rad[base * 3 + e] = ind[e]; }
 }
 
-// The whole job. q0/qd0/qdd0: this world's initial state.
-AD void reach_job(Ctx& x, const RobotParams& rp, int T, int t, const double* q0, const double* qd0, const double* qdd0,
-                  const ReachOut& out, long j, JrsJoint* jrs, double* scratch) {
-    const int NJ = rp.num_joints;
-    // ---- JRS (Trajectory.cu:63-254): scalars in parallel, PZs by thread 0 ----
-    for (int i = x.g.tid; i < NF; i += x.g.n) jrs[i] = jrs_joint(rp, T, t, i, q0[i], qd0[i], qdd0[i]);
-    x.g.sync();
+T0FN void t0_emit_torque(Ctx& x, const ReachOut& out, long j, int a, int i, double* rdist, double* ured) {
+    const PZH& h = x.H[a];
+    const long base = j * NF + i;
+    // disturbance u_int - u_nom: centres and monomials cancel exactly, the independent parts add
+    // (armour_main.cu:135-137, PZsparse.cu:813-834)
+    rdist[i] = h.ind[1][0] + h.ind[0][0];
+    // reduce (PZsparse.cu:352-368)
+    double ind = h.ind[0][0];
+    int kk = 0;
+    for (int k = 0; k < h.cnt; k++) {
+        const uint64_t hh = x.A->h[h.hoff + k];
+        double c = x.A->c[h.coff + (long)k * h.stride + (h.comp >= 0 ? h.comp : 0)];
+        if (h.scaled) c = h.scale * c;
+        if (hh < HASH_K_ONLY) {
+            if (kk < CAP_UM) {
+                out.tq_hash[base * CAP_UM + kk] = (uint16_t)hh;
+                out.tq_coef[base * CAP_UM + kk] = c;
+            } else {
+                *x.err |= ERR_OUTCAP;
+            }
+            kk++;
+        } else {
+            ind += fabs(c);
+        }
+    }
+    out.tq_cnt[base] = kk < CAP_UM ? kk : CAP_UM;
+    out.tq_center[base] = h.center[0];
+    out.tq_rad[base] = ind;
+    ured[i] = ind;
+}
+
+// torque radius (armour_main.cu:173-211)
+T0FN void t0_torque_radius(const RobotParams& rp, const ReachOut& out, long j, const double* rdist, const double* ured) {
+    const double ubc = rp.alpha * (rp.M_max - rp.M_min) * rp.eps;
+    double tr[NF];
+    Ival rho = Ival{0.0, 0.0};
     for (int i = 0; i < NF; i++) {
-        const JrsJoint& J = jrs[i];
-        uint64_t hh[4];
-        double cf[4][9];
-        // qd / qda / qdda 1-D PZs: k_i and qde_i / qdae_i / qddae_i monomials
-        for (int v = 0; v < 3; v++) {
-            const double c0 = v == 2 ? J.qdd_c : J.qd_c;
-            hh[0] = slot_hash(SLOT_K + i);
-            cf[0][0] = v == 2 ? J.qdd_k : J.qd_k;
-            hh[1] = slot_hash((v == 0 ? SLOT_QDE : v == 1 ? SLOT_QDAE : SLOT_QDDAE) + i);
-            cf[1][0] = v == 0 ? J.qd_e : v == 1 ? J.qda_e : J.qdd_e;
-            h_make_raw(x, (v == 0 ? hs::QD0 : v == 1 ? hs::QDA0 : hs::QDD0) + i, 1, 1, &c0, 2, hh, cf);
-        }
-        if (rp.axes[i] != 0) {
-            // rotation PZ about the joint axis (PZsparse.cu:179-205 + makeRotationMatrix :211-250)
-            const int ax = rp.axes[i];
-            double cen[9];
-            for (int e = 0; e < 9; e++) cen[e] = (e % 4 == 0) ? 1.0 : 0.0;
-            auto put = [&](double* Rm, double c, double s) {
-                const double ns = -1.0 * s;
-                if (ax == 1) { Rm[1 + 3] = c; Rm[1 + 6] = ns; Rm[2 + 3] = s; Rm[2 + 6] = c; }
-                else if (ax == 2) { Rm[0] = c; Rm[0 + 6] = s; Rm[2] = ns; Rm[2 + 6] = c; }
-                else { Rm[0] = c; Rm[0 + 3] = ns; Rm[1] = s; Rm[1 + 3] = c; }
-            };
-            put(cen, J.cos_c, J.sin_c);
-            for (int m = 0; m < 4; m++) for (int e = 0; e < 9; e++) cf[m][e] = 0.0;
-            put(cf[0], J.cos_k, 0.0); hh[0] = slot_hash(SLOT_K + i);
-            put(cf[1], J.cos_e, 0.0); hh[1] = slot_hash(SLOT_COS + i);
-            put(cf[2], 0.0, J.sin_k); hh[2] = slot_hash(SLOT_K + i);
-            put(cf[3], 0.0, J.sin_e); hh[3] = slot_hash(SLOT_SIN + i);
-            h_make_raw(x, hs::T1, 3, 3, cen, 4, hh, cf);
-            h_const(x, hs::T2, 3, 3, rp.rpy[i], 0.0);
-            op_mul(x, hs::R0 + i, hs::T2, hs::T1);
-        } else {
-            h_const(x, hs::R0 + i, 3, 3, rp.rpy[i], 0.0);
-        }
-        op_transpose(x, hs::RT0 + i, hs::R0 + i);
+        const Ival tmp = iv(0.0 - rdist[i], 0.0 + rdist[i]);
+        rho = iadd(rho, imul(tmp, tmp));
+        tr[i] = ubc + 0.5 * fmax(fabs(tmp.lo), fabs(tmp.hi));
     }
-    for (int i = NF; i < NJ; i++) {
-        h_const(x, hs::R0 + i, 3, 3, rp.rpy[i], 0.0);
-        op_transpose(x, hs::RT0 + i, hs::R0 + i);
-    }
-    h_const(x, hs::R0 + NJ, 3, 3, rp.rpy[MAX_J], 0.0);  // PZsparse(0, 0, 0)
+    rho = isqrt(rho);
+    for (int i = 0; i < NF; i++) tr[i] += 0.5 * rho.hi;
+    for (int i = 0; i < NF; i++) tr[i] += ured[i];
+    for (int i = 0; i < NF; i++) tr[i] += rp.friction[i];
+    for (int i = 0; i < NF; i++) out.torque_radius[j * NF + i] = tr[i];
+}
 
-    // ---- forward kinematics (Dynamics.cu:69-81) + reduce_link_PZ (armour_main.cu:124-126) ----
-    {
-        const int FKR = hs::W, FKT = hs::WDOT, P = hs::T1, TMP = hs::T2, BOX = hs::T3;
-        h_const(x, FKR, 3, 3, rp.rpy[MAX_J], 0.0);
-        h_zero(x, FKT, 3, 1);
-        for (int i = 0; i < NJ; i++) {
-            h_const(x, P, 3, 1, &rp.trans[3 * i], 0.0);
-            op_mul(x, TMP, FKR, P);
-            op_add(x, FKT, FKT, TMP, +1);
-            op_mul(x, FKR, FKR, hs::R0 + i);
-            // link box: generators on the qde_0 / qdae_0 / qddae_0 slots (Dynamics.cu:98-116)
-            uint64_t hh[4];
-            double cf[4][9];
-            for (int m = 0; m < 3; m++) {
-                for (int e = 0; e < 9; e++) cf[m][e] = 0.0;
-                cf[m][m] = rp.link_g[i][m];
-                hh[m] = slot_hash(NF * (m + 1));
-            }
-            h_make_raw(x, BOX, 3, 1, rp.link_c[i], 3, hh, cf);
-            op_mul(x, TMP, FKR, BOX);
-            op_add(x, hs::T7, TMP, FKT, +1);
-            emit_link(x, out, j, i);
-        }
-    }
+// ---- operator dispatch ----------------------------------------------------------------------
+// number of candidate terms of a simplifying op (uniform: every thread reads the same headers)
+AI int op_terms(const Ctx& x, const Op& op) {
+    const PZH& A = x.H[op.a];
+    const PZH& B = x.H[op.b];
+    if (op.code == OP_MUL) return A.cnt + B.cnt + A.cnt * B.cnt;
+    if (op.code == OP_STACK3) return A.cnt + B.cnt + x.H[op.c].cnt;
+    return A.cnt + B.cnt;
+}
 
-    // ---- RNEA, nominal and interval fused (Dynamics.cu:83-181) ----
-    h_zero(x, hs::W, 3, 1);
-    h_zero(x, hs::WDOT, 3, 1);
-    h_zero(x, hs::WAUX, 3, 1);
-    h_zero(x, hs::LIN, 3, 1);
-    if (x.g.tid == 0) x.H[hs::LIN].center[2] = rp.gravity;
-    x.g.sync();
-    for (int i = 0; i < NJ; i++) {
-        const int RT = hs::RT0 + i;
-        const double* p = &rp.trans[3 * i];
-        const double* c = &rp.com[3 * i];
-        // line 16
-        op_cross_pm(x, hs::T1, hs::WDOT, p, hs::CA);
-        op_add(x, hs::T2, hs::LIN, hs::T1, +1);
-        op_cross_pm(x, hs::T3, hs::WAUX, p, hs::CB);
-        op_cross_pp(x, hs::T4, hs::W, hs::T3, hs::CA);
-        op_add(x, hs::T5, hs::T2, hs::T4, +1);
-        op_mul(x, hs::LIN, RT, hs::T5);
-        // line 13
-        op_mul(x, hs::W, RT, hs::W);
-        if (rp.axes[i] != 0) {
-            const int ax = (rp.axes[i] < 0 ? -rp.axes[i] : rp.axes[i]) - 1;
-            op_add_one_dim(x, hs::W, hs::W, hs::QD0 + i, ax, 0);
-            op_mul(x, hs::WAUX, RT, hs::WAUX);
-            op_mul(x, hs::WDOT, RT, hs::WDOT);
-            h_zero(x, hs::T1, 3, 1);
-            op_add_one_dim(x, hs::T1, hs::T1, hs::QD0 + i, ax, 0);
-            op_cross_pp(x, hs::T2, hs::WAUX, hs::T1, hs::CA);
-            op_add(x, hs::WDOT, hs::WDOT, hs::T2, +1);
-            op_add_one_dim(x, hs::WDOT, hs::WDOT, hs::QDD0 + i, ax, 0);
-            op_add_one_dim(x, hs::WAUX, hs::WAUX, hs::QDA0 + i, ax, 0);
-        } else {
-            op_mul(x, hs::WAUX, RT, hs::WAUX);
-            op_mul(x, hs::WDOT, RT, hs::WDOT);
-        }
-        // line 23 & 27
-        op_cross_pm(x, hs::T1, hs::WDOT, c, hs::CA);
-        op_add(x, hs::T2, hs::LIN, hs::T1, +1);
-        op_cross_pm(x, hs::T3, hs::WAUX, c, hs::CB);
-        op_cross_pp(x, hs::T4, hs::W, hs::T3, hs::CA);
-        op_add(x, hs::T5, hs::T2, hs::T4, +1);
-        {
-            double m = rp.mass[i];
-            h_const(x, hs::T6, 1, 1, &m, rp.mass_uncertainty);
-        }
-        op_mul(x, hs::F0 + i, hs::T6, hs::T5);
-        // line 29
-        h_const(x, hs::T6, 3, 3, &rp.inertia[i * 9], rp.inertia_uncertainty);
-        op_mul(x, hs::T1, hs::T6, hs::WDOT);
-        op_mul(x, hs::T2, hs::T6, hs::W);
-        op_cross_pp(x, hs::T3, hs::WAUX, hs::T2, hs::CA);
-        op_add(x, hs::N0 + i, hs::T1, hs::T3, +1);
+// term list of a simplifying op (all threads, uniform)
+AI void op_terms_of(const Ctx& x, const Op& op, Terms& T) {
+    switch (op.code) {
+        case OP_MUL: terms_mul(x, op.a, op.b, T); break;
+        case OP_ADD: terms_add(x, op.a, op.b, op.i, T); break;
+        case OP_STACK3: terms_stack3(x, op.a, op.b, op.c, T); break;
+        default: terms_add_one_dim(x, op.a, op.b, op.i, T); break;
     }
-    h_zero(x, hs::FF, 3, 1);
-    h_zero(x, hs::NN, 3, 1);
+}
+// output header (thread 0)
+AI void op_header(Ctx& x, const Op& op, const Terms& T) {
+    switch (op.code) {
+        case OP_MUL: header_mul(x, op.o, op.a, op.b, T); break;
+        case OP_ADD: header_add(x, op.o, op.a, op.b, op.i); break;
+        case OP_STACK3: header_stack3(x, op.o, op.a, op.b, op.c); break;
+        default: header_add_one_dim(x, op.o, op.a, op.b, op.i); break;
+    }
+}
+
+// One job (world w, interval t): the interpreter. jrs / scratch live in LDS.
+// dump (diagnostics, may be null): per op, the output handle's [cnt, R*C, centre[0..2], ind0[0],
+// ind1[0], absum[0]] after the op
+constexpr int DUMP_W = 8;
+AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int T, int t, const double* q0,
+                    const double* qd0, const double* qdd0, const ReachOut& out, long j, JrsJoint* jrs,
+                    double* scratch, unsigned long long* prof, double* dump = nullptr) {
+    const int tid = x.g.tid;
     double* rdist = scratch;
     double* ured = scratch + NF;
-    for (int i = NJ - 1; i >= 0; i--) {
-        const int R1 = hs::R0 + i + 1;
-        // line 29: n = N + R*n + cross(com, F) + cross(p_{i+1}, R*f); R*f evaluated once
-        op_mul(x, hs::T1, R1, hs::NN);
-        op_add(x, hs::T2, hs::N0 + i, hs::T1, +1);
-        op_cross_mp(x, hs::T3, &rp.com[3 * i], hs::F0 + i, hs::CA);
-        op_add(x, hs::T4, hs::T2, hs::T3, +1);
-        op_mul(x, hs::T5, R1, hs::FF);
-        op_cross_mp(x, hs::T6, &rp.trans[3 * (i + 1)], hs::T5, hs::CA);
-        op_add(x, hs::NN, hs::T4, hs::T6, +1);
-        // line 28
-        op_add(x, hs::FF, hs::T5, hs::F0 + i, +1);
-        if (rp.axes[i] != 0 && i < NF) {
-            const int ax = (rp.axes[i] < 0 ? -rp.axes[i] : rp.axes[i]) - 1;
-            h_elem(x, hs::T1, hs::NN, ax, 0);
-            h_scale(x, hs::T2, rp.armature[i], hs::QDD0 + i);
-            op_add(x, hs::T3, hs::T1, hs::T2, +1);
-            h_scale(x, hs::T2, rp.damping[i], hs::QD0 + i);
-            op_add(x, hs::T7, hs::T3, hs::T2, +1);
-            emit_torque(x, out, j, i, rdist, ured);
+    for (int pc = 0; pc < nops; pc++) {
+        const Op op = prog[pc];
+#if defined(__HIP_DEVICE_COMPILE__)
+        long long c0 = 0;
+        if (prof && tid == 0) c0 = clock64();
+#endif
+        switch (op.code) {
+            case OP_JRS:
+                for (int i = tid; i < NF; i += x.g.n) jrs[i] = jrs_joint(rp, T, t, i, q0[i], qd0[i], qdd0[i]);
+                break;
+            case OP_MAKE1D: if (tid == 0) t0_make_1d(x, op.o, jrs[op.i], op.i, op.b); break;
+            case OP_MAKEROT: if (tid == 0) t0_make_rot(x, op.o, rp, jrs[op.i], op.i); break;
+            case OP_MAKEBOX: if (tid == 0) t0_make_box(x, op.o, rp, op.i); break;
+            case OP_CONST:
+                if (tid == 0) {
+                    if (op.a == CONST_RPY) t0_const(x, op.o, 3, 3, rp.rpy[op.i], 0.0);
+                    else if (op.a == CONST_TRANS) t0_const(x, op.o, 3, 1, &rp.trans[3 * op.i], 0.0);
+                    else if (op.a == CONST_MASS) t0_const(x, op.o, 1, 1, &rp.mass[op.i], rp.mass_uncertainty);
+                    else t0_const(x, op.o, 3, 3, &rp.inertia[9 * op.i], rp.inertia_uncertainty);
+                }
+                break;
+            case OP_ZERO:
+                if (tid == 0) {
+                    hdr_init(x.H[op.o], op.b, op.c);
+                    if (op.i) x.H[op.o].center[2] = rp.gravity;
+                }
+                break;
+            case OP_VIEW: if (tid == 0) t0_view(x, op.o, op.a, op.i, op.b, op.s); break;
+            case OP_TRANSPOSE: if (tid == 0) t0_transpose(x, op.o, op.a); break;
+            case OP_EMIT_LINK: if (tid == 0) t0_emit_link(x, out, j, op.a, op.i); break;
+            case OP_EMIT_TORQUE: if (tid == 0) t0_emit_torque(x, out, j, op.a, op.i, rdist, ured); break;
+            case OP_TORQUE_RADIUS: if (tid == 0) t0_torque_radius(rp, out, j, rdist, ured); break;
+            default: {
+                // MUL / ADD / STACK3 / ADD1D: term list, header, simplify
+                Terms Tm;
+                op_terms_of(x, op, Tm);
+                const int N = op_terms(x, op);
+                if (tid == 0) op_header(x, op, Tm);
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (N <= 64 && !(x.mode & 1)) {
+                    if (tid < 64) simplify_small(x, op.o, Tm, N);
+                    break;
+                }
+                long long pt = (x.phase && tid == 0) ? clock64() : 0;
+#endif
+                stage_sources(x, Tm);
+                x.g.sync();
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (x.phase && tid == 0) atomicAdd(&x.phase[6], (unsigned long long)(clock64() - pt));
+#endif
+                simplify_big(x, op.o, Tm, N);
+                break;
+            }
         }
+        if (op.sync) x.g.sync();
+        if (dump && op.o >= 0) {
+            x.g.sync();
+            if (tid == 0) {
+                const PZH& h = x.H[op.o];
+                double* d = dump + (long)pc * DUMP_W;
+                d[0] = h.cnt; d[1] = h.R * h.C; d[2] = h.center[0]; d[3] = h.center[1]; d[4] = h.center[2];
+                d[5] = h.ind[0][0]; d[6] = h.ind[1][0]; d[7] = h.absum[0];
+            }
+            x.g.sync();
+        }
+#if defined(__HIP_DEVICE_COMPILE__)
+        if (prof && tid == 0) {
+            atomicAdd(&prof[2 * pc], (unsigned long long)(clock64() - c0));
+            if (op.code >= OP_MUL && op.code <= OP_ADD1D) atomicAdd(&prof[2 * pc + 1], (unsigned long long)op_terms(x, op));
+        }
+#endif
+    }
+}
+
+// ---- host: program builder --------------------------------------------------------------------
+struct ProgramBuilder {
+    std::vector<Op> ops;
+    std::vector<int> free_slots;
+    int nslots = 0;
+
+    int alloc() {
+        if (!free_slots.empty()) { const int s = free_slots.back(); free_slots.pop_back(); return s; }
+        return nslots++;
+    }
+    void rel(int s) { free_slots.push_back(s); }
+    void rel(std::initializer_list<int> l) { for (int s : l) rel(s); }
+    void emit(int code, int o = -1, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
+        Op op;
+        op.code = code; op.o = o; op.a = a; op.b = b; op.c = c; op.i = i; op.s = s; op.sync = 1; op.pad = 0;
+        ops.push_back(op);
+    }
+    int out(int code, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
+        const int o = alloc();
+        emit(code, o, a, b, c, i, s);
+        return o;
+    }
+    int mul(int a, int b) { return out(OP_MUL, a, b); }
+    int add(int a, int b) { return out(OP_ADD, a, b, 0, +1); }
+    int sub(int a, int b) { return out(OP_ADD, a, b, 0, -1); }
+    int stack3(int a, int b, int c) { return out(OP_STACK3, a, b, c); }
+    int add1d(int self, int a, int e) { return out(OP_ADD1D, self, a, 0, e); }
+    int elem(int a, int e) { return out(OP_VIEW, a, 0, 0, e); }
+    int scaled_elem(int a, int e, double s) { return out(OP_VIEW, a, 1, 0, e, s); }
+    int scaled(int a, double s) { return out(OP_VIEW, a, 1, 0, -1, s); }
+    int cnst(int kind, int i) { return out(OP_CONST, kind, 0, 0, i); }
+    int zero(int R, int C, int gravity = 0) { return out(OP_ZERO, 0, R, C, gravity); }
+
+    // cross products (PZsparse.cu:1118-1167), component by component as the reference does
+    int cross_pm(int a, const double* b) {  // PZ x const
+        const int s0 = scaled_elem(a, 1, b[2]), s1 = scaled_elem(a, 2, b[1]);
+        const int r0 = sub(s0, s1);
+        rel({s0, s1});
+        const int s2 = scaled_elem(a, 2, b[0]), s3 = scaled_elem(a, 0, b[2]);
+        const int r1 = sub(s2, s3);
+        rel({s2, s3});
+        const int s4 = scaled_elem(a, 0, b[1]), s5 = scaled_elem(a, 1, b[0]);
+        const int r2 = sub(s4, s5);
+        rel({s4, s5});
+        const int o = stack3(r0, r1, r2);
+        rel({r0, r1, r2});
+        return o;
+    }
+    int cross_mp(const double* a, int b) {  // const x PZ
+        const int s0 = scaled_elem(b, 2, a[1]), s1 = scaled_elem(b, 1, a[2]);
+        const int r0 = sub(s0, s1);
+        rel({s0, s1});
+        const int s2 = scaled_elem(b, 0, a[2]), s3 = scaled_elem(b, 2, a[0]);
+        const int r1 = sub(s2, s3);
+        rel({s2, s3});
+        const int s4 = scaled_elem(b, 1, a[0]), s5 = scaled_elem(b, 0, a[1]);
+        const int r2 = sub(s4, s5);
+        rel({s4, s5});
+        const int o = stack3(r0, r1, r2);
+        rel({r0, r1, r2});
+        return o;
+    }
+    int cross_pp(int a, int b) {  // PZ x PZ
+        const int a0 = elem(a, 0), a1 = elem(a, 1), a2 = elem(a, 2);
+        const int b0 = elem(b, 0), b1 = elem(b, 1), b2 = elem(b, 2);
+        int p = mul(a1, b2), q = mul(a2, b1);
+        const int r0 = sub(p, q);
+        rel({p, q});
+        p = mul(a2, b0); q = mul(a0, b2);
+        const int r1 = sub(p, q);
+        rel({p, q});
+        p = mul(a0, b1); q = mul(a1, b0);
+        const int r2 = sub(p, q);
+        rel({p, q, a0, a1, a2, b0, b1, b2});
+        const int o = stack3(r0, r1, r2);
+        rel({r0, r1, r2});
+        return o;
     }
 
-    // ---- torque radius (armour_main.cu:173-211) ----
-    if (x.g.tid == 0) {
-        const double ubc = rp.alpha * (rp.M_max - rp.M_min) * rp.eps;
-        double tr[NF];
-        Ival rho = Ival{0.0, 0.0};
+    // the whole job, op for op KPR/Trajectory.cu:63-254, Dynamics.cu:69-181, armour_main.cu:118-211
+    void build(const RobotParams& rp) {
+        const int NJ = rp.num_joints;
+        int R[MAX_J + 1], RT[MAX_J], QD[NF], QDA[NF], QDD[NF];
+        emit(OP_JRS);
         for (int i = 0; i < NF; i++) {
-            const Ival tmp = iv(0.0 - rdist[i], 0.0 + rdist[i]);
-            rho = iadd(rho, imul(tmp, tmp));
-            tr[i] = ubc + 0.5 * fmax(fabs(tmp.lo), fabs(tmp.hi));
+            QD[i] = out(OP_MAKE1D, 0, 0, 0, i);
+            QDA[i] = out(OP_MAKE1D, 0, 1, 0, i);
+            QDD[i] = out(OP_MAKE1D, 0, 2, 0, i);
+            if (rp.axes[i] != 0) {
+                const int rot = out(OP_MAKEROT, 0, 0, 0, i);
+                const int c = cnst(CONST_RPY, i);
+                R[i] = mul(c, rot);
+                rel({rot, c});
+            } else {
+                R[i] = cnst(CONST_RPY, i);
+            }
+            RT[i] = out(OP_TRANSPOSE, R[i]);
         }
-        rho = isqrt(rho);
-        for (int i = 0; i < NF; i++) tr[i] += 0.5 * rho.hi;
-        for (int i = 0; i < NF; i++) tr[i] += ured[i];
-        for (int i = 0; i < NF; i++) tr[i] += rp.friction[i];
-        for (int i = 0; i < NF; i++) out.torque_radius[j * NF + i] = tr[i];
+        for (int i = NF; i < NJ; i++) {
+            R[i] = cnst(CONST_RPY, i);
+            RT[i] = out(OP_TRANSPOSE, R[i]);
+        }
+        R[NJ] = cnst(CONST_RPY, MAX_J);  // PZsparse(0, 0, 0)
+
+        // forward kinematics (Dynamics.cu:69-81) + reduce_link_PZ (armour_main.cu:124-126)
+        {
+            int FKR = cnst(CONST_RPY, MAX_J), FKT = zero(3, 1);
+            for (int i = 0; i < NJ; i++) {
+                const int P = cnst(CONST_TRANS, i);
+                const int tmp = mul(FKR, P);
+                const int fkt = add(FKT, tmp);
+                rel({P, tmp, FKT});
+                FKT = fkt;
+                const int fkr = mul(FKR, R[i]);
+                rel(FKR);
+                FKR = fkr;
+                const int box = out(OP_MAKEBOX, 0, 0, 0, i);
+                const int tmp2 = mul(FKR, box);
+                const int link = add(tmp2, FKT);
+                emit(OP_EMIT_LINK, -1, link, 0, 0, i);
+                rel({box, tmp2, link});
+            }
+            rel({FKR, FKT});
+        }
+
+        // RNEA, nominal and interval fused (Dynamics.cu:83-181)
+        int W = zero(3, 1), WDOT = zero(3, 1), WAUX = zero(3, 1), LIN = zero(3, 1, 1);
+        int F[MAX_J], N[MAX_J];
+        for (int i = 0; i < NJ; i++) {
+            const double* p = &rp.trans[3 * i];
+            const double* c = &rp.com[3 * i];
+            // line 16
+            {
+                const int t1 = cross_pm(WDOT, p);
+                const int t2 = add(LIN, t1);
+                const int t3 = cross_pm(WAUX, p);
+                const int t4 = cross_pp(W, t3);
+                const int t5 = add(t2, t4);
+                const int lin = mul(RT[i], t5);
+                rel({t1, t2, t3, t4, t5, LIN});
+                LIN = lin;
+            }
+            // line 13
+            {
+                int w = mul(RT[i], W);
+                rel(W);
+                W = w;
+            }
+            if (rp.axes[i] != 0) {
+                const int ax = (rp.axes[i] < 0 ? -rp.axes[i] : rp.axes[i]) - 1;
+                int w = add1d(W, QD[i], ax);
+                rel(W);
+                W = w;
+                const int waux = mul(RT[i], WAUX);
+                rel(WAUX);
+                WAUX = waux;
+                const int wdot = mul(RT[i], WDOT);
+                rel(WDOT);
+                WDOT = wdot;
+                const int z = zero(3, 1);
+                const int t1 = add1d(z, QD[i], ax);
+                const int t2 = cross_pp(WAUX, t1);
+                const int wd2 = add(WDOT, t2);
+                rel({z, t1, t2, WDOT});
+                WDOT = add1d(wd2, QDD[i], ax);
+                rel(wd2);
+                const int wa2 = add1d(WAUX, QDA[i], ax);
+                rel(WAUX);
+                WAUX = wa2;
+            } else {
+                const int waux = mul(RT[i], WAUX);
+                rel(WAUX);
+                WAUX = waux;
+                const int wdot = mul(RT[i], WDOT);
+                rel(WDOT);
+                WDOT = wdot;
+            }
+            // line 23 & 27
+            {
+                const int t1 = cross_pm(WDOT, c);
+                const int t2 = add(LIN, t1);
+                const int t3 = cross_pm(WAUX, c);
+                const int t4 = cross_pp(W, t3);
+                const int t5 = add(t2, t4);
+                const int m = cnst(CONST_MASS, i);
+                F[i] = mul(m, t5);
+                rel({t1, t2, t3, t4, t5, m});
+            }
+            // line 29
+            {
+                const int I = cnst(CONST_INERTIA, i);
+                const int t1 = mul(I, WDOT);
+                const int t2 = mul(I, W);
+                const int t3 = cross_pp(WAUX, t2);
+                N[i] = add(t1, t3);
+                rel({I, t1, t2, t3});
+            }
+        }
+        rel({W, WDOT, WAUX, LIN});
+        int FF = zero(3, 1), NN = zero(3, 1);
+        for (int i = NJ - 1; i >= 0; i--) {
+            // line 29: n = N + R*n + cross(com, F) + cross(p_{i+1}, R*f); R*f evaluated once
+            const int t1 = mul(R[i + 1], NN);
+            const int t2 = add(N[i], t1);
+            const int t3 = cross_mp(&rp.com[3 * i], F[i]);
+            const int t4 = add(t2, t3);
+            const int t5 = mul(R[i + 1], FF);
+            const int t6 = cross_mp(&rp.trans[3 * (i + 1)], t5);
+            const int nn = add(t4, t6);
+            rel({t1, t2, t3, t4, t6, NN});
+            NN = nn;
+            // line 28
+            const int ff = add(t5, F[i]);
+            rel({t5, FF});
+            FF = ff;
+            if (rp.axes[i] != 0 && i < NF) {
+                const int ax = (rp.axes[i] < 0 ? -rp.axes[i] : rp.axes[i]) - 1;
+                const int e = elem(NN, ax);
+                const int s1 = scaled(QDD[i], rp.armature[i]);
+                const int u1 = add(e, s1);
+                const int s2 = scaled(QD[i], rp.damping[i]);
+                const int u = add(u1, s2);
+                emit(OP_EMIT_TORQUE, -1, u, 0, 0, i);
+                rel({e, s1, u1, s2, u});
+            }
+        }
+        emit(OP_TORQUE_RADIUS);
+        // thread-0 ops chained back to back need no barrier between them
+        auto t0_only = [](int c) {
+            return c == OP_MAKE1D || c == OP_MAKEROT || c == OP_MAKEBOX || c == OP_CONST || c == OP_ZERO ||
+                   c == OP_VIEW || c == OP_TRANSPOSE || c == OP_EMIT_LINK || c == OP_EMIT_TORQUE;
+        };
+        for (size_t k = 0; k + 1 < ops.size(); k++)
+            if (t0_only(ops[k].code) && t0_only(ops[k + 1].code)) ops[k].sync = 0;
     }
-    x.g.sync();
-}
+};
 
 }  // namespace armour

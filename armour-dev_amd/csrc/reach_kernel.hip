@@ -1,20 +1,23 @@
 // armour-mi355x — reach-set kernel: one 256-thread workgroup per (world, time interval) job.
-// Persistent grid: each workgroup walks jobs job = blockIdx.x + k * gridDim.x and owns a private
-// HBM arena (monomial storage) and a global fallback sort buffer for products larger than the
-// LDS key buffer. LDS (~61 KB) holds the PZ handle table and the (hash, index) sort keys, so two
-// workgroups fit per CU.
+// Persistent grid: each workgroup walks jobs job = blockIdx.x + k * gridDim.x, interprets the
+// reach program (reach.h) for each, and owns a private HBM arena (monomial storage) plus a global
+// fallback sort buffer for products larger than the LDS key buffer. LDS (~78 KB) holds the PZ
+// handle table, the (hash, index) keys and the operand staging buffer, so two workgroups fit per CU.
 #include "reach.h"
 
 namespace armour {
 
 constexpr int REACH_THREADS = 256;
 constexpr int KEY_CAP_LDS = 2048;
+constexpr int STAGE_DOUBLES = 2560;
 
 struct ReachArgs {
     int W, T;
     const double* q0;    // [W][NF]
     const double* qd0;
     const double* qdd0;
+    const Op* prog;      // reach program (device copy of ProgramBuilder::ops)
+    int nops;
     uint64_t* arena_h;   // [grid][arena_cap]
     double* arena_c;     // [grid][arena_cap * 3]
     long arena_cap;
@@ -22,15 +25,20 @@ struct ReachArgs {
     uint32_t* gki;
     int* gkp;
     int gcap;
+    unsigned long long* bytes;  // algorithmic monomial bytes of all jobs (one atomic per job)
+    unsigned long long* prof;   // optional per-op [cycles, terms] (null: off)
+    int mode;                   // engine diagnostics (Ctx::mode)
+    double* dump;               // optional op-by-op state of job 0 (null: off)
 };
 
 __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
-    __shared__ PZH H[hs::COUNT];
+    __shared__ PZH H[MAX_SLOTS];
     __shared__ uint64_t kh[KEY_CAP_LDS];
     __shared__ uint32_t ki[KEY_CAP_LDS];
     __shared__ int kp[KEY_CAP_LDS];
-    __shared__ double red[(REACH_THREADS / 64) * 9];
-    __shared__ int iscan[2 * REACH_THREADS];
+    __shared__ double stage[STAGE_DOUBLES];
+    __shared__ double red[(REACH_THREADS / 64) * 18];
+    __shared__ int iscan[REACH_THREADS / 64];
     __shared__ Arena arena;
     __shared__ int err;
     __shared__ JrsJoint jrs[NF];
@@ -41,17 +49,20 @@ __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotPara
     Ctx x;
     x.g = Grp{(int)threadIdx.x, (int)blockDim.x};
     x.H = H;
-    x.opa = hs::OPA; x.opb = hs::OPB; x.opc = hs::OPC;
     x.A = &arena;
     x.kh = kh; x.ki = ki; x.kp = kp; x.cap_lds = KEY_CAP_LDS;
     x.gkh = a.gkh + (long)blockIdx.x * a.gcap;
     x.gki = a.gki + (long)blockIdx.x * a.gcap;
     x.gkp = a.gkp + (long)blockIdx.x * a.gcap;
     x.cap_glb = a.gcap;
+    x.stage = stage;
+    x.stage_cap = STAGE_DOUBLES;
     x.red = red;
     x.iscan = iscan;
     x.err = &err;
     x.thr = rp.simplify_threshold;
+    x.phase = a.prof ? a.prof + 2 * a.nops : nullptr;
+    x.mode = a.mode;
 
     const long njobs = (long)a.W * a.T;
     for (long job = blockIdx.x; job < njobs; job += gridDim.x) {
@@ -63,6 +74,7 @@ __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotPara
             arena.ccap = a.arena_cap * 3;
             arena.hused = 0;
             arena.cused = 0;
+            arena.bytes = 0;
             err = 0;
         }
         if (threadIdx.x < NF) {
@@ -71,8 +83,12 @@ __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotPara
             qdd0s[threadIdx.x] = a.qdd0[w * NF + threadIdx.x];
         }
         __syncthreads();
-        reach_job(x, rp, a.T, t, q0s, qd0s, qdd0s, out, job, jrs, scratch);
-        if (threadIdx.x == 0 && err) atomicOr(&out.err[w], err);
+        run_program(x, rp, a.prog, a.nops, a.T, t, q0s, qd0s, qdd0s, out, job, jrs, scratch, a.prof,
+                    job == 0 ? a.dump : nullptr);
+        if (threadIdx.x == 0) {
+            if (err) atomicOr(&out.err[w], err);
+            atomicAdd(a.bytes, (unsigned long long)arena.bytes);
+        }
         __syncthreads();
     }
 }

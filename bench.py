@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Benchmark: ARMOUR planning iterations/sec (Kinova 7-DOF, 100 time steps, 20 obstacles).
+
+Metric (BASELINE.json): planning iterations/sec at 1/2/4/8 GPUs. One planning iteration = one
+complete plan of KPR/armour_main.cu (JRS -> PZ FK/RNEA -> torque radius -> hyperplanes -> NLP to
+termination -> feasibility re-check). A step = one batch of `--batch` synthetic random-obstacle
+worlds planned on each GPU (weak scaling: every rank plans its own worlds); after each step the
+per-world records (k_opt, cost, feasible) are all-gathered over RCCL and rank 0 takes the argmin
+over feasible worlds (the only collective on this path).
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
+       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "armour-dev_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=256, help="worlds per GPU per step")
+    ap.add_argument("--T", type=int, default=100)
+    ap.add_argument("--O", type=int, default=20)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
+    return ap.parse_args()
+
+
+def cpu_baseline(worlds, T, seconds):
+    """Oracle (CPU restatement of the reference path, oracle/) on the host cores: whole plans of
+    the same worlds until `seconds` of work, OpenMP threads = the box's CPU share (<= 16)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OraclePlanner  # test/baseline infrastructure only
+
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    done, t0 = 0, time.perf_counter()
+    for w in worlds:
+        P = OraclePlanner(*w, T=T, threads=threads)
+        P.reach()
+        P.plan()
+        done += 1
+        if time.perf_counter() - t0 > seconds and done >= 2:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=done / dt, unit="plans/s", cores=threads, kind="port",
+                sample=f"{done} full plans (oracle C++ restatement, T={T}, O={len(worlds[0][4])}) in {dt:.1f}s")
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != a.gpus and a.gpus > 1:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world_size}", file=sys.stderr)
+    dist = None
+    if world_size > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist_mod.init_process_group("nccl", rank=rank, world_size=world_size)
+        dist = dist_mod
+
+    import armour_amd as A
+
+    worlds = [A.make_world(rank * a.batch + i, a.O) for i in range(a.batch)]
+    planner = A.Planner(T=a.T, max_obstacles=a.O, max_worlds=a.batch, device=local_rank)
+
+    def gather(res):
+        rec = np.array([[*r["k_opt"], r["cost"], float(r["feasible"]), float(r["status"])] for r in res])
+        if dist is None:
+            allrec = rec
+        else:
+            import torch
+
+            t = torch.from_numpy(rec).cuda()
+            out = [torch.empty_like(t) for _ in range(world_size)]
+            dist.all_gather(out, t)
+            allrec = torch.cat(out).cpu().numpy()
+        feas = allrec[:, 8] > 0.5
+        best = int(np.argmin(np.where(feas, allrec[:, 7], np.inf))) if feas.any() else -1
+        return allrec, best
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        res, tm = planner.plan(worlds)
+        gather(res)
+    barrier()
+    t0 = time.perf_counter()
+    tms = []
+    for _ in range(a.steps):
+        res, tm = planner.plan(worlds)
+        allrec, best = gather(res)
+        tms.append(tm)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    total_plans = a.steps * a.batch * world_size
+    # roofline of the dominant kernel (reach_kernel): algorithmic bytes = monomial bytes read and
+    # written by the PZ operators, timed with HIP events on the planner stream
+    rk_ms = float(np.mean([t["reach_kernel_ms"] for t in tms]))
+    rk_bytes = float(np.mean([t["reach_bytes"] for t in tms]))
+    achieved = rk_bytes / (rk_ms * 1e-3) / 1e9
+    n_feas = int(allrec[:, 8].sum())
+    line = {
+        "metric": "planning iterations/sec (7-DOF, 100 t-steps, 20 obs)",
+        "value": total_plans / elapsed,
+        "unit": "plans/s",
+        "n_gpus": world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic random-obstacle worlds (armour_amd.worlds, seeds rank*batch+i)",
+        "config": {"workload": f"Kinova Gen3 7-DOF, T={a.T}, O={a.O} box obstacles, {a.batch} worlds/GPU/step",
+                   "num_time_steps": a.T, "obstacles": a.O, "worlds_per_gpu": a.batch,
+                   "parallelism": f"world-sharded x{world_size}, RCCL all_gather of per-world records"},
+        "breakdown_ms": {"reach": float(np.mean([t["reach_ms"] for t in tms])),
+                         "nlp": float(np.mean([t["nlp_ms"] for t in tms])),
+                         "reach_kernel": rk_ms},
+        "feasible_worlds": n_feas,
+        "total_worlds_last_step": int(allrec.shape[0]),
+        "roofline": {"kernel": "reach_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+        "cpu_baseline": None,
+    }
+    if a.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_baseline(worlds, a.T, a.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

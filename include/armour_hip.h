@@ -66,6 +66,8 @@ typedef struct armour_timing {
     double reach_ms;     /* JRS + PZ FK/RNEA + torque radius + hyperplanes */
     double nlp_ms;       /* solver */
     double total_ms;     /* incl. host<->device copies of inputs and results */
+    double reach_kernel_ms; /* reach_kernel alone (hipEvents around its launch) */
+    double reach_bytes;  /* algorithmic monomial bytes the PZ operators read + wrote */
 } armour_timing;
 
 armour_planner* armour_create(const armour_config* cfg);
@@ -93,6 +95,19 @@ int armour_get_link_centers(armour_planner* p, int w, double* centers);       /*
 int armour_get_link_generators(armour_planner* p, int w, double* gens);       /* [T][NJ][3][6] */
 int armour_get_torque_radius(armour_planner* p, int w, double* radius);       /* [T][7] */
 int armour_num_joints(const armour_planner* p);
+
+/* Diagnostics (no reference counterpart). The reach kernel interprets a fixed op program built
+ * from the robot tables; these expose it for profiling. armour_get_reach_program writes the op
+ * codes (if capacity >= count) and returns the op count. armour_get_reach_profile writes
+ * [cycles, terms] per op accumulated over all jobs when the environment variable
+ * ARMOUR_PROFILE_OPS was set at armour_create, followed by 8 phase counters of the large-operator
+ * path (capacity counts pairs: >= op count + 4), and returns the op count. */
+int armour_get_reach_program(const armour_planner* p, int* codes, int capacity);
+int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms, int capacity);
+/* op-by-op state of job 0 (world 0, t = 0) of the last reach: per op 8 doubles [monomial count,
+ * block size, centre[0..2], nominal ind[0], interval ind[0], sum|m|[0]] of the op's output, when
+ * ARMOUR_DUMP_OPS was set at armour_create; returns the op count. */
+int armour_get_reach_dump(armour_planner* p, double* dump, int capacity);
 
 #ifdef __cplusplus
 }

@@ -9,37 +9,45 @@
 
 using namespace armour;
 
+static double* g_dump = nullptr;
+extern "C" void emu_set_dump(double* d) { g_dump = d; }
 extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, const double* qdd0,
                          double* link_gens, double* link_center, double* link_rad, int* link_cnt,
                          uint16_t* link_hash, double* link_coef, double* tq_center, double* tq_rad,
                          int* tq_cnt, uint16_t* tq_hash, double* tq_coef, double* torque_radius,
-                         long* arena_used) {
+                         long* arena_used, double* arena_bytes, int* nops, int* nslots) {
     static RobotParams rp;
     static bool init = false;
     if (!init) { kinova_gen3(rp); init = true; }
+    static ProgramBuilder pb;
+    if (pb.ops.empty()) pb.build(rp);
     const long cap = 1 << 22;
     std::vector<uint64_t> ah(cap);
     std::vector<double> ac(cap * 3);
-    std::vector<PZH> H(hs::COUNT);
+    std::vector<PZH> H(pb.nslots);
     const int kcap = 1 << 16;
     std::vector<uint64_t> kh(kcap);
     std::vector<uint32_t> ki(kcap);
     std::vector<int> kp(kcap);
-    double red[9 * 4];
+    double red[18];
     int iscan[2];
-    Arena A{ah.data(), ac.data(), cap, cap * 3, 0, 0};
+    Arena A{ah.data(), ac.data(), cap, cap * 3, 0, 0, 0.0};
     int err = 0;
     Ctx x;
     x.g = Grp{0, 1};
     x.H = H.data();
-    x.opa = hs::OPA; x.opb = hs::OPB; x.opc = hs::OPC;
     x.A = &A;
     x.kh = kh.data(); x.ki = ki.data(); x.kp = kp.data(); x.cap_lds = kcap;
     x.gkh = kh.data(); x.gki = ki.data(); x.gkp = kp.data(); x.cap_glb = kcap;
+    std::vector<double> stage(4096);
+    x.stage = stage.data();
+    x.stage_cap = 4096;
     x.red = red;
     x.iscan = iscan;
     x.err = &err;
     x.thr = rp.simplify_threshold;
+    x.phase = nullptr;
+    x.mode = 0;
     int werr = 0;
     ReachOut out;
     out.T = 1;
@@ -50,7 +58,10 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     out.tq_rad = tq_rad; out.torque_radius = torque_radius; out.err = &werr;
     JrsJoint jrs[NF];
     double scratch[2 * NF];
-    reach_job(x, rp, T, t, q0, qd0, qdd0, out, 0, jrs, scratch);
+    run_program(x, rp, pb.ops.data(), (int)pb.ops.size(), T, t, q0, qd0, qdd0, out, 0, jrs, scratch, nullptr, g_dump);
     *arena_used = A.hused;
+    if (arena_bytes) *arena_bytes = A.bytes;
+    if (nops) *nops = (int)pb.ops.size();
+    if (nslots) *nslots = pb.nslots;
     return err;
 }
