@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 from .robots import KINOVA
-from .worlds import example_world, make_world
+from .worlds import csv_world, example_world, make_world, straight_line_waypoint
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libarmour_hip.so")
@@ -66,6 +66,7 @@ def lib():
         L.armour_reach_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Timing)]
         L.armour_eval_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
         L.armour_get_reach_program.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.armour_get_joint_bounds.argtypes = [ctypes.c_void_p, _dp]
         L.armour_get_reach_dump.argtypes = [ctypes.c_void_p, _dp, ctypes.c_int]
         L.armour_get_reach_profile.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
         for name in ("armour_get_constraints", "armour_get_link_centers", "armour_get_link_generators",
@@ -79,7 +80,7 @@ def lib():
 ABI_SYMBOLS = ["armour_create", "armour_destroy", "armour_last_error", "armour_num_constraints",
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
-               "armour_num_joints", "armour_get_reach_program", "armour_get_reach_profile",
+               "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
                "armour_get_reach_dump"]
 
 
@@ -172,6 +173,13 @@ class Planner:
         _check(lib().armour_get_link_generators(self.h, w, _ptr(g)))
         return g
 
+    def joint_bounds(self):
+        """the 28 trailing values of armour_constraints.out: per joint [lb + qe, ub - qe], then
+        per joint [-v + qde, v - qde]"""
+        b = np.zeros(28)
+        _check(lib().armour_get_joint_bounds(self.h, _ptr(b)))
+        return b
+
     def reach_program(self):
         """op codes of the reach kernel's program (diagnostics)"""
         n = lib().armour_get_reach_program(self.h, None, 0)
@@ -205,4 +213,4 @@ class Planner:
         return r
 
 
-__all__ = ["Planner", "ArmourError", "make_world", "example_world", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]
+__all__ = ["Planner", "ArmourError", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]

@@ -106,3 +106,31 @@ EXAMPLE_OBSTACLES = np.array(_EX_ROWS + _EX_ROWS, dtype=np.float64)
 def example_world():
     z = np.zeros(7)
     return EXAMPLE_Q0.copy(), z.copy(), z.copy(), EXAMPLE_QDES.copy(), EXAMPLE_OBSTACLES.copy()
+
+
+def straight_line_waypoint(q_cur, q_goal, lookahead=0.1, robot: Robot = KINOVA):
+    """q_des of the straight-line high-level planner (simulator/planners/high_level_planners/
+    robot_arm_straight_line_HLP.m:45-57; lookahead 0.1 as kinova_src/scripts/
+    kinova_run_100_worlds.m:57): a step of `lookahead` toward the goal, angle-wrapped on the
+    continuous joints."""
+    q_cur = np.asarray(q_cur, dtype=np.float64)
+    d = np.asarray(q_goal, dtype=np.float64) - q_cur
+    cont = robot.state_lb <= -1000.0
+    d[cont] = (d[cont] + np.pi) % (2 * np.pi) - np.pi
+    return q_cur + lookahead * d / np.linalg.norm(d)
+
+
+def csv_world(rows, robot: Robot = KINOVA):
+    """Planning problem of a saved world (kinova_src/saved_worlds/random/*.csv, read as
+    kinova_simulator_interfaces/kinova_scenarios/load_saved_world.m: row 1 start, row 2 goal,
+    rows 4.. box obstacles [centre(3), side lengths(3)]): the first replan from rest with the
+    straight-line waypoint as q_des. Obstacles become zonotopes with generators diag(side / 2)
+    (simulator/worlds/obstacles/box_obstacle_zonotope.m)."""
+    rows = np.asarray(rows, dtype=np.float64)
+    start, goal = rows[0, :7], rows[1, :7]
+    obs = []
+    for r in rows[3:]:
+        c, side = r[:3], r[3:6]
+        obs.append(np.concatenate([c, np.diag(side / 2).T.reshape(-1)]))
+    z = np.zeros(7)
+    return start.copy(), z.copy(), z.copy(), straight_line_waypoint(start, goal, robot=robot), np.array(obs)

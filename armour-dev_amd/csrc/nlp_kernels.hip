@@ -174,8 +174,10 @@ __device__ double wrap_to_pi(double a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// g(x) and dense Jacobian. grid (T, W); mode 0: all worlds at ws.x into slot 0;
-// mode 1: searching worlds at ws.xt into slot 1 - cur
+// g(x) and dense Jacobian, grid (T, W). mode 0: ws.x into slot 0 (start point,
+// armour_eval_constraints); mode 1: the line-search trial ws.xt into the non-current slot (worlds
+// still searching only); mode 2: ws.x into the non-current slot, so the link centres hold the
+// final iterate's values
 __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) {
     const int t = blockIdx.x, w = blockIdx.y;
     WorldState& S = d.ws[w];
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     __shared__ double x[NF];
     __shared__ double lc[MAX_J][3];
     __shared__ double dlc[MAX_J][NF][3];
-    if (threadIdx.x < NF) x[threadIdx.x] = mode == 0 ? S.x[threadIdx.x] : S.xt[threadIdx.x];
+    if (threadIdx.x < NF) x[threadIdx.x] = mode == 1 ? S.xt[threadIdx.x] : S.x[threadIdx.x];
     __syncthreads();
     const long jt = (long)w * d.T + t;
     // link slices: one thread per (link, component)  (PZsparse.cu:404-435, 477-516)

@@ -310,6 +310,8 @@ static int run_solver(armour_planner* p) {
         HIPCK(hipStreamSynchronize(p->stream));
         if (p->h_flags[1] == 0) break;  // every world converged, hit the cap or failed
     }
+    // sliced link centres at the final iterate (armour_joint_position_center.out payload)
+    hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 2);
     hipLaunchKernelGGL(feasible_kernel, dim3(W), dim3(256), 0, p->stream, d, p->feas);
     HIPCK(hipGetLastError());
     return 0;
@@ -348,6 +350,18 @@ void armour_destroy(armour_planner* p) {
 
 int armour_num_constraints(const armour_planner* p, int O) { return p ? NF * p->T + p->T * p->NJ * O + NF * 4 : ARMOUR_E_ARG; }
 int armour_num_joints(const armour_planner* p) { return p ? p->NJ : ARMOUR_E_ARG; }
+
+int armour_get_joint_bounds(const armour_planner* p, double* b) {
+    if (!p || !b) return fail(ARMOUR_E_ARG, "null argument");
+    const RobotParams& rp = p->rp;
+    for (int i = 0; i < NF; i++) {
+        b[2 * i] = rp.state_lb[i] + rp.qe;
+        b[2 * i + 1] = rp.state_ub[i] - rp.qe;
+        b[2 * NF + 2 * i] = -rp.speed_limits[i] + rp.qde;
+        b[2 * NF + 2 * i + 1] = rp.speed_limits[i] - rp.qde;
+    }
+    return 0;
+}
 
 int armour_reach_batch(armour_planner* p, int W, const armour_world* worlds, armour_timing* timing) {
     if (!p) return fail(ARMOUR_E_ARG, "null planner");

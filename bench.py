@@ -78,24 +78,14 @@ def main():
         dist = dist_mod
 
     import armour_amd as A
+    from armour_amd import dist as D
 
-    worlds = [A.make_world(rank * a.batch + i, a.O) for i in range(a.batch)]
+    # weak scaling: rank r plans worlds r*batch .. r*batch+batch-1 (armour_amd.dist.shard of the whole job)
+    worlds = [A.make_world(i, a.O) for i in D.shard(a.batch * world_size, rank, world_size)]
     planner = A.Planner(T=a.T, max_obstacles=a.O, max_worlds=a.batch, device=local_rank)
 
     def gather(res):
-        rec = np.array([[*r["k_opt"], r["cost"], float(r["feasible"]), float(r["status"])] for r in res])
-        if dist is None:
-            allrec = rec
-        else:
-            import torch
-
-            t = torch.from_numpy(rec).cuda()
-            out = [torch.empty_like(t) for _ in range(world_size)]
-            dist.all_gather(out, t)
-            allrec = torch.cat(out).cpu().numpy()
-        feas = allrec[:, 8] > 0.5
-        best = int(np.argmin(np.where(feas, allrec[:, 7], np.inf))) if feas.any() else -1
-        return allrec, best
+        return D.gather(D.records(res), dist, device="cuda" if dist is not None else None)
 
     def barrier():
         if dist is not None:

@@ -91,10 +91,14 @@ int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g
 
 /* Outputs of world w of the last batch (the armour_*.out payloads, armour_main.cu:340-398) */
 int armour_get_constraints(armour_planner* p, int w, double* g);              /* m values at k_opt */
-int armour_get_link_centers(armour_planner* p, int w, double* centers);       /* [T][NJ][3] sliced */
+int armour_get_link_centers(armour_planner* p, int w, double* centers);       /* [T][NJ][3] sliced at the
+                                                                               last evaluated point: k_opt after a plan */
 int armour_get_link_generators(armour_planner* p, int w, double* gens);       /* [T][NJ][3][6] */
 int armour_get_torque_radius(armour_planner* p, int w, double* radius);       /* [T][7] */
 int armour_num_joints(const armour_planner* p);
+/* the 28 trailing values of armour_constraints.out (armour_main.cu:385-396): per joint
+ * [lb + qe, ub - qe] then per joint [-v + qde, v - qde] */
+int armour_get_joint_bounds(const armour_planner* p, double* bounds28);
 
 /* Diagnostics (no reference counterpart). The reach kernel interprets a fixed op program built
  * from the robot tables; these expose it for profiling. armour_get_reach_program writes the op

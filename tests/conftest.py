@@ -1,0 +1,49 @@
+"""Shared test setup.
+
+`-m "not gpu"` (runs in the build container): the oracle against the golden fixtures and its own
+properties, the host emulation of the reach program against the oracle, the C ABI's exports, and
+the distributed host logic on gloo. `-m gpu` (MI355X): the HIP path through the C ABI against the
+oracle and the fixtures. The oracle (oracle/) is the checker only.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "armour-dev_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); runs the product library")
+
+
+def _ensure(lib, target_dir):
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", target_dir], check=True, capture_output=True)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def built_checkers():
+    """The checkers (oracle, host emulation) are cheap to build; make sure they exist."""
+    _ensure(os.path.join(ROOT, "oracle", "liboracle.so"), os.path.join(ROOT, "oracle"))
+    _ensure(os.path.join(ROOT, "tests", "emu", "libreach_emu.so"), os.path.join(ROOT, "tests", "emu"))
+
+
+def golden_names():
+    import json
+
+    return json.load(open(os.path.join(GOLDEN, "index.json")))["fixtures"]
+
+
+def load_golden(name):
+    import numpy as np
+
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def world_of(fx):
+    return fx["q0"], fx["qd0"], fx["qdd0"], fx["q_des"], fx["obstacles"]

@@ -1,0 +1,38 @@
+"""TEST HARNESS — ctypes wrapper of tests/emu/libreach_emu.so (sequential host emulation of the
+reach kernel's op program, armour-dev_amd/csrc/reach.h)."""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NJ, CAP_LM, CAP_UM = 7, 64, 256
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        _L = ctypes.CDLL(os.path.join(HERE, "libreach_emu.so"))
+    return _L
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def reach_job(world, T, t):
+    """Outputs of job (world, t) as the kernel writes them."""
+    q0, qd0, qdd0 = [np.ascontiguousarray(np.asarray(a, dtype=np.float64)) for a in world[:3]]
+    o = dict(link_gens=np.zeros((NJ, 18)), link_center=np.zeros((NJ, 3)), link_rad=np.zeros((NJ, 3)),
+             link_cnt=np.zeros(NJ, np.int32), link_hash=np.zeros((NJ, CAP_LM), np.uint16),
+             link_coef=np.zeros((NJ, CAP_LM, 3)), tq_center=np.zeros(7), tq_rad=np.zeros(7),
+             tq_cnt=np.zeros(7, np.int32), tq_hash=np.zeros((7, CAP_UM), np.uint16), tq_coef=np.zeros((7, CAP_UM)),
+             torque_radius=np.zeros(7))
+    used, bts, nops, nsl = ctypes.c_long(), ctypes.c_double(), ctypes.c_int(), ctypes.c_int()
+    order = ["link_gens", "link_center", "link_rad", "link_cnt", "link_hash", "link_coef", "tq_center", "tq_rad",
+             "tq_cnt", "tq_hash", "tq_coef", "torque_radius"]
+    err = lib().emu_reach(T, t, _p(q0), _p(qd0), _p(qdd0), *[_p(o[k]) for k in order], ctypes.byref(used),
+                          ctypes.byref(bts), ctypes.byref(nops), ctypes.byref(nsl))
+    o.update(err=err, arena=used.value, bytes=bts.value, nops=nops.value, nslots=nsl.value)
+    return o

@@ -1,0 +1,88 @@
+"""The drop-in boundary: libarmour_hip.so exports exactly the C ABI include/armour_hip.h declares
+(no compute calls here — the build container has no GPU), the Python binding knows every entry,
+the product never reaches into the oracle, and without a device the product fails loudly."""
+import os
+import re
+import subprocess
+
+import pytest
+
+import armour_amd as A
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "armour_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(armour_\w+)\s*\(", src)))
+
+
+def exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if " T " in l}
+
+
+@pytest.fixture(scope="module")
+def lib_path():
+    if not os.path.exists(A.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "armour-dev_amd", "csrc"), "../armour_amd/libarmour_hip.so"],
+                       check=True, capture_output=True)
+    return A.LIB_PATH
+
+
+def test_header_symbols_exported(lib_path):
+    funcs = header_functions()
+    assert len(funcs) >= 15
+    missing = set(funcs) - exported(lib_path)
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    assert sorted(A.ABI_SYMBOLS) == header_functions()
+
+
+def test_library_loads_and_binds(lib_path):
+    L = A.lib()
+    for name in A.ABI_SYMBOLS:
+        assert hasattr(L, name)
+
+
+def test_no_cpu_fallback_in_product():
+    """The product path never imports or links the oracle / emulation."""
+    pkg = os.path.join(ROOT, "armour-dev_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".h", ".hip", ".cpp", "Makefile")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert "import oracle" not in text and "from oracle" not in text and "liboracle" not in text, f
+                assert "reach_emu" not in text, f
+
+
+def test_executable_built():
+    exe = os.path.join(ROOT, "armour-dev_amd", "armour_amd", "armour_main")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "armour-dev_amd", "csrc")], check=True, capture_output=True)
+    assert os.access(exe, os.X_OK)
+    assert "armour_plan_batch" in subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True,
+                                                 text=True).stdout
+
+
+def test_create_without_device_fails_loudly():
+    """No GPU (this container): armour_create fails with a message instead of computing on the CPU."""
+    try:
+        import torch
+
+        if torch.cuda.device_count() > 0:
+            pytest.skip("a device is present")
+    except ImportError:
+        pass
+    with pytest.raises(A.ArmourError):
+        A.Planner(T=10, max_obstacles=2, max_worlds=1)
+
+
+def test_bad_config_rejected_before_device():
+    """Argument checks come first (KPR/Parameters.h: NUM_TIME_STEPS must be even)."""
+    with pytest.raises(A.ArmourError, match="even"):
+        A.Planner(T=11, max_obstacles=2, max_worlds=1)

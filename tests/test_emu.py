@@ -1,0 +1,55 @@
+"""The reach kernel's op program (armour-dev_amd/csrc/reach.h: ProgramBuilder + interpreter +
+pz_engine.h), run by the sequential host emulation, against the oracle: monomial structure must
+be identical (same hashes, same counts) and values equal to rounding."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "emu"))
+import emu  # noqa: E402
+
+from armour_amd.worlds import example_world, make_world  # noqa: E402
+from oracle import OraclePlanner  # noqa: E402
+
+T = 100
+CASES = [("random0", make_world(0, 20), [0, 37, 99]), ("random7", make_world(7, 20), [1, 50]),
+         ("example", example_world(), [0, 63])]
+
+
+@pytest.mark.parametrize("name,world,ts", CASES, ids=[c[0] for c in CASES])
+def test_emulated_program_matches_oracle(name, world, ts):
+    P = OraclePlanner(*world, T=T, threads=4)
+    P.reach()
+    lg_o = P.get(0).reshape(T, 7, 18)
+    tr_o = P.torque_radius()
+    for t in ts:
+        o = emu.reach_job(world, T, t)
+        assert o["err"] == 0
+        np.testing.assert_allclose(o["link_gens"], lg_o[t], rtol=0, atol=1e-14)
+        np.testing.assert_allclose(o["torque_radius"], tr_o[t], rtol=0, atol=1e-12)
+        for l in range(7):
+            pz = P.pz(0, l * T + t)
+            n = o["link_cnt"][l]
+            assert n == len(pz["hashes"])
+            np.testing.assert_array_equal(o["link_hash"][l, :n], pz["hashes"])
+            np.testing.assert_allclose(o["link_coef"][l, :n], pz["coeffs"], rtol=0, atol=1e-14)
+            np.testing.assert_allclose(o["link_center"][l], pz["center"], rtol=0, atol=1e-14)
+            np.testing.assert_allclose(o["link_rad"][l], pz["indep"], rtol=0, atol=1e-14)
+        for j in range(7):
+            pz = P.pz(1, j * T + t)
+            n = o["tq_cnt"][j]
+            assert n == len(pz["hashes"])
+            np.testing.assert_array_equal(o["tq_hash"][j, :n], pz["hashes"])
+            np.testing.assert_allclose(o["tq_coef"][j, :n], pz["coeffs"][:, 0], rtol=0, atol=1e-13)
+            np.testing.assert_allclose(o["tq_center"][j], pz["center"][0], rtol=0, atol=1e-12)
+            np.testing.assert_allclose(o["tq_rad"][j], pz["indep"][0], rtol=0, atol=1e-12)
+
+
+def test_program_shape():
+    """The program fits the kernel's handle table and its arena/byte counters are sane."""
+    o = emu.reach_job(make_world(0, 20), T, 50)
+    assert o["nslots"] <= 72 and o["nops"] > 1000
+    assert 0 < o["arena"] < (1 << 17)
+    assert o["bytes"] > 0

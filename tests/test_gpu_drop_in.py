@@ -1,0 +1,83 @@
+"""The drop-in executable armour_main speaks the reference's file protocol
+(kinova_planner_realtime/armour_main.cu:5-10, 37-77, 319-398)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import armour_amd as A
+from armour_amd.robots import KINOVA
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "armour-dev_amd", "armour_amd", "armour_main")
+
+
+def write_input(path, world):
+    """the writer of KSI/uarmtd_planner.m:169-196 (%.10f, space separated)"""
+    q0, qd0, qdd0, qdes, obs = world
+    with open(os.path.join(path, "armour.in"), "w") as f:
+        for v in (q0, qd0, qdd0, qdes):
+            f.write(" ".join(f"{x:.10f}" for x in v) + "\n")
+        f.write(f"{len(obs)}\n")
+        for o in obs:
+            f.write(" ".join(f"{x:.10f}" for x in o) + "\n")
+
+
+def run(path, T):
+    env = dict(os.environ, ARMOUR_NUM_TIME_STEPS=str(T))
+    return subprocess.run([EXE, path], env=env, capture_output=True, text=True, timeout=300)
+
+
+def test_example_world_protocol(tmp_path):
+    T = 20
+    world = A.example_world()
+    write_input(str(tmp_path), world)
+    r = run(str(tmp_path), T)
+    assert r.returncode == 0, r.stderr
+    out = [float(v) for v in open(tmp_path / "armour.out").read().split()]
+    # the same problem through the library (inputs rounded as the text file carries them)
+    rounded = [np.round(np.asarray(a, dtype=np.float64), 10) for a in world]
+    P = A.Planner(T=T, max_obstacles=10, max_worlds=1)
+    res, _ = P.plan([tuple(rounded)])
+    if res[0]["feasible"]:
+        assert len(out) == 8
+        np.testing.assert_allclose(out[:7], res[0]["k_opt"], rtol=1e-9, atol=1e-9)
+    else:
+        assert out[0] == -1 and len(out) == 2
+    NJ = 7
+    c = np.loadtxt(tmp_path / "armour_joint_position_center.out")
+    assert c.shape == (T * NJ, 3)
+    np.testing.assert_allclose(c.reshape(T, NJ, 3), P.link_centers(0), rtol=1e-9, atol=1e-9)
+    g = np.loadtxt(tmp_path / "armour_joint_position_radius.out")
+    assert g.shape == (T * NJ * 3, 6)
+    np.testing.assert_allclose(g.reshape(T, NJ, 3, 6), P.link_generators(0), rtol=1e-9, atol=1e-12)
+    u = np.loadtxt(tmp_path / "armour_control_input_radius.out")
+    assert u.shape == (T, 7)
+    np.testing.assert_allclose(u, P.torque_radius(0), rtol=1e-9)
+    cons = np.loadtxt(tmp_path / "armour_constraints.out")
+    m = P.num_constraints(10)
+    assert cons.shape == (m + 28,)
+    np.testing.assert_allclose(cons[:m], P.constraints(0), rtol=1e-5, atol=1e-5)
+    b = P.joint_bounds()
+    np.testing.assert_allclose(cons[m:], b, rtol=1e-5)
+    # per joint [lb + qe, ub - qe], then [-v + qde, v - qde] (armour_main.cu:385-396)
+    assert np.all(b[0:14:2] > KINOVA.state_lb) and np.all(b[1:14:2] < KINOVA.state_ub)
+    np.testing.assert_allclose(b[14::2], -b[15::2])
+    assert np.all(b[15::2] < KINOVA.speed_limits)
+
+
+def test_missing_input_fails_like_reference(tmp_path):
+    r = run(str(tmp_path), 10)
+    assert r.returncode != 0
+    assert open(tmp_path / "armour.out").read().split() == ["-1"]
+
+
+def test_too_many_obstacles_fails_like_reference(tmp_path):
+    world = A.make_world(0, 3)
+    q0, qd0, qdd0, qdes, obs = world
+    write_input(str(tmp_path), (q0, qd0, qdd0, qdes, np.tile(obs, (14, 1))))  # 42 > MAX_OBSTACLE_NUM
+    r = run(str(tmp_path), 10)
+    assert r.returncode != 0
+    assert open(tmp_path / "armour.out").read().split() == ["-1"]

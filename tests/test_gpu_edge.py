@@ -1,0 +1,65 @@
+"""Edge cases of the boundary on the GPU: no obstacles, MAX_OBSTACLE_NUM obstacles, single-world
+and full batches, argument and state errors, outputs at the solution."""
+import numpy as np
+import pytest
+
+import armour_amd as A
+from oracle import OraclePlanner
+
+pytestmark = pytest.mark.gpu
+
+
+def test_no_obstacles():
+    T = 20
+    world = A.make_world(4, 0)
+    P = A.Planner(T=T, max_obstacles=0, max_worlds=1)
+    res, _ = P.plan([world])
+    R = OraclePlanner(*world, T=T, threads=4)
+    R.reach()
+    ro = R.plan()
+    assert P.num_constraints(0) == 7 * T + 28
+    assert res[0]["feasible"] == ro["feasible"]
+    np.testing.assert_allclose(res[0]["k_opt"], ro["k_opt"], rtol=0, atol=1e-8)
+
+
+def test_max_obstacles_and_full_batch():
+    T, O, W = 10, 40, 3
+    worlds = [A.make_world(30 + s, O) for s in range(W)]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    res, _ = P.plan(worlds)
+    for w, world in enumerate(worlds):
+        R = OraclePlanner(*world, T=T, threads=4)
+        R.reach()
+        ro = R.plan()
+        assert res[w]["feasible"] == ro["feasible"]
+        np.testing.assert_allclose(res[w]["k_opt"], ro["k_opt"], rtol=0, atol=1e-8)
+
+
+def test_outputs_at_solution():
+    """armour_joint_position_center.out / armour_constraints.out payloads are those at k_opt"""
+    T, O = 20, 5
+    world = A.make_world(8, O)
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=1)
+    res, _ = P.plan([world])
+    k = res[0]["k_opt"]
+    R = OraclePlanner(*world, T=T, threads=4)
+    R.reach()
+    g, _, lc = R.eval(k, centers=True)
+    np.testing.assert_allclose(P.link_centers(0), lc, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(P.constraints(0), g, rtol=0, atol=1e-9)
+
+
+def test_argument_and_state_errors():
+    P = A.Planner(T=10, max_obstacles=3, max_worlds=2)
+    with pytest.raises(A.ArmourError, match="state|no reach|plan"):
+        P.constraints(0)
+    worlds = [A.make_world(s, 3) for s in range(3)]
+    with pytest.raises(A.ArmourError, match="num_worlds"):
+        P.plan(worlds)                      # more worlds than max_worlds
+    with pytest.raises(A.ArmourError, match="max_obstacles"):
+        P.plan([A.make_world(0, 4)])        # more obstacles than max_obstacles
+    with pytest.raises(A.ArmourError, match="same num_obstacles"):
+        P.plan([A.make_world(0, 3), A.make_world(1, 2)])
+    P.plan(worlds[:2])
+    with pytest.raises(A.ArmourError, match="out of range"):
+        P.torque_radius(2)

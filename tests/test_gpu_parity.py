@@ -1,0 +1,100 @@
+"""HIP path (libarmour_hip.so through the C ABI) against the golden fixtures and a fresh oracle.
+
+Tolerances (fp64 throughout; north_star: "constraints within 1e-9, collision decisions
+bit-exact"): reach-set outputs and constraints/Jacobian 1e-9 absolute (observed ~1e-14); the
+solver's k_opt 1e-8 with identical iteration counts and feasibility; every collision decision
+(g > 1e-4, NLPclass.cu:472-484) and the feasibility re-check exactly equal.
+"""
+import numpy as np
+import pytest
+
+import armour_amd as A
+from conftest import golden_names, load_golden, world_of
+from oracle import OraclePlanner
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+COL_THR = 1e-4  # COLLISION_AVOIDANCE_CONSTRAINT_VIOLATION_THRESHOLD (Parameters.h:38)
+
+
+def collision_rows(T, O):
+    return slice(7 * T, 7 * T + 7 * T * O)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_fixture(name):
+    fx = load_golden(name)
+    T, O = int(fx["T"]), fx["obstacles"].shape[0]
+    P = A.Planner(T=T, max_obstacles=max(O, 1), max_worlds=1)
+    world = world_of(fx)
+    P.reach([world])
+    np.testing.assert_allclose(P.torque_radius(0), fx["torque_radius"], rtol=0, atol=TOL)
+    np.testing.assert_allclose(P.link_generators(0), fx["link_gens"], rtol=0, atol=TOL)
+    chk = OraclePlanner(*world, T=T, threads=2)  # feasibility decision of the GPU's g
+    chk.reach()
+    if "x" in fx:
+        for x, g0, J0, f0 in zip(fx["x"], fx["g"], fx["J"], fx["feasible_at_x"]):
+            g, J = P.eval_constraints(0, x)
+            np.testing.assert_allclose(g, g0, rtol=0, atol=TOL)
+            np.testing.assert_allclose(J, J0, rtol=0, atol=TOL)
+            cr = collision_rows(T, O)
+            np.testing.assert_array_equal(g[cr] > COL_THR, g0[cr] > COL_THR)
+            assert chk.feasible(g) == bool(f0)
+    res, tm = P.plan([world])
+    r = res[0]
+    assert r["feasible"] == bool(fx["feasible"])
+    assert r["iterations"] == int(fx["iterations"]) and r["status"] == int(fx["status"])
+    np.testing.assert_allclose(r["k_opt"], fx["k_opt"], rtol=0, atol=1e-8)
+    np.testing.assert_allclose(r["cost"], fx["cost"], rtol=1e-8, atol=1e-12)
+    np.testing.assert_allclose(P.constraints(0), fx["g_opt"], rtol=0, atol=1e-7)
+    assert tm["reach_kernel_ms"] > 0 and tm["reach_bytes"] > 0
+
+
+def _compare_batch(T, O, seeds, xs):
+    worlds = [A.make_world(s, O) for s in seeds]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
+    P.reach(worlds)
+    refs = []
+    for w, world in enumerate(worlds):
+        R = OraclePlanner(*world, T=T, threads=8)
+        R.reach()
+        refs.append(R)
+        np.testing.assert_allclose(P.torque_radius(w), R.torque_radius(), rtol=0, atol=TOL)
+        np.testing.assert_allclose(P.link_generators(w), R.link_gens(), rtol=0, atol=TOL)
+        for x in xs:
+            g, J = P.eval_constraints(w, x)
+            go, Jo = R.eval(x)
+            np.testing.assert_allclose(g, go, rtol=0, atol=TOL)
+            np.testing.assert_allclose(J, Jo, rtol=0, atol=TOL)
+            cr = collision_rows(T, O)
+            np.testing.assert_array_equal(g[cr] > COL_THR, go[cr] > COL_THR)
+            assert R.feasible(g) == R.feasible(go)
+    res, _ = P.plan(worlds)
+    for r, R in zip(res, refs):
+        ro = R.plan()
+        assert r["feasible"] == ro["feasible"] and r["iterations"] == ro["iterations"]
+        np.testing.assert_allclose(r["k_opt"], ro["k_opt"], rtol=0, atol=1e-8)
+
+
+def test_config2_batch():
+    """BASELINE configs[1]: Kinova, T=100, O=20"""
+    _compare_batch(100, 20, [11, 12, 13, 14], [np.zeros(7), np.array([0.5, 0.6, 0.7, 0.0, -0.5, -0.6, -0.7])])
+
+
+def test_config3_batch():
+    """BASELINE configs[2]: T=200, O=40 (MAX_OBSTACLE_NUM)"""
+    _compare_batch(200, 40, [21, 22], [np.full(7, -0.4)])
+
+
+def test_batch_position_and_rerun_are_bitwise_stable():
+    T, O = 20, 6
+    worlds = [A.make_world(s, O) for s in range(5)]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=5)
+    res_a, _ = P.plan(worlds)
+    g_a = [P.constraints(w) for w in range(5)]
+    res_b, _ = P.plan(worlds[::-1])
+    res_c, _ = P.plan(worlds)
+    for w in range(5):
+        assert np.array_equal(res_a[w]["k_opt"], res_b[4 - w]["k_opt"])
+        assert np.array_equal(res_a[w]["k_opt"], res_c[w]["k_opt"])
+        assert np.array_equal(g_a[w], P.constraints(w))
