@@ -245,9 +245,6 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             if (ls + 1 < opt.max_ls) alpha *= 0.5;
         }
         if (accepted && !ftype) { filt_theta.push_back((1 - 1e-5) * theta0); filt_phi.push_back(phi0 - 1e-8 * theta0); }
-        const double nu = 0, D = Dphi, f_dbg = f; (void)f_dbg;
-        nfail = accepted ? 0 : nfail + 1;
-        if (getenv("IPM_DEBUG")) fprintf(stderr, "it %d mu %.2e E0 %.3e infd %.2e infp %.2e c0 %.2e ap %.3e ad %.3e alpha %.3e acc %d nu %.2e f %.5f rp1 %.3e D %.3e |dx| %.3e\n", it, mu, E0, inf_d, inf_p, compl0, ap, ad, alpha, (int)accepted, nu, f, rp1, D, std::sqrt(dx[0]*dx[0]+dx[1]*dx[1]+dx[2]*dx[2]+dx[3]*dx[3]+dx[4]*dx[4]+dx[5]*dx[5]+dx[6]*dx[6]));
         // 6. accept the trial point; multipliers with kappa_sigma safeguard
         double wa_new[NMAX] = {0};
         for (int r = 0; r < R; r++) {

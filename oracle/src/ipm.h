@@ -11,7 +11,8 @@
 //   2. monotone barrier update mu <- max(tol/10, min(kappa_mu*mu, mu^theta)) while E_mu <= kappa_eps*mu
 //   3. Newton step on the reduced 7x7 system (H + sum_k sigma_k a_k a_k^T) dx = -grad f + sum_k a_k (mu/s_k - sigma_k r_p,k)
 //   4. ds, dz, fraction-to-boundary step sizes
-//   5. backtracking line search on phi = f - mu sum ln s + nu ||c(x) - s||_1
+//   5. Ipopt's filter line search (no restoration phase) on theta = ||c(x) - s||_1 and the
+//      barrier objective phi = f - mu sum ln s, at most max_ls backtracking trials
 //   6. multiplier update with Ipopt's kappa_sigma safeguard; damped BFGS update of H
 #pragma once
 
