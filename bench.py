@@ -60,6 +60,20 @@ def cpu_baseline(worlds, T, seconds):
                 sample=f"{done} full plans (oracle C++ restatement, T={T}, O={len(worlds[0][4])}) in {dt:.1f}s")
 
 
+def traffic_record(T, O, batch):
+    """HBM traffic per reach_kernel launch from the newest committed PMC summary of the same
+    workload (profiles/r*_reach_traffic.json, made by tools/gpu_prof.sh + tools/pmc_traffic.py:
+    separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected); None if there is none."""
+    import glob
+
+    best = None
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_reach_traffic.json"))):
+        rec = json.load(open(fn))
+        if rec.get("config") == dict(T=T, O=O, batch=batch):
+            best = (fn, rec)
+    return best
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -144,9 +158,14 @@ def main():
         "feasible_worlds": n_feas,
         "total_worlds_last_step": int(allrec.shape[0]),
         "roofline": {"kernel": "reach_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": rk_bytes, "launch_ms": rk_ms},
         "cpu_baseline": None,
     }
+    tr = traffic_record(a.T, a.O, a.batch)
+    if tr is not None:
+        line["roofline"]["traffic"] = tr[1]["traffic_bytes_per_launch"]
+        line["roofline"]["traffic_source"] = os.path.relpath(tr[0], ROOT)
     if a.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(worlds, a.T, a.cpu_seconds)
     print(json.dumps(line), flush=True)
