@@ -197,13 +197,13 @@ class Planner:
         return d
 
     def reach_profile(self):
-        """([nops, 2] accumulated (cycles, terms) per op, [8] large-op phase cycles);
+        """([nops, 2] accumulated (cycles, terms) per op, [16] phase cycles);
         needs ARMOUR_PROFILE_OPS at creation"""
         n = lib().armour_get_reach_profile(self.h, None, 0)
         if n < 0:
             _check(n)
-        buf = (ctypes.c_ulonglong * (2 * n + 8))()
-        _check(min(0, lib().armour_get_reach_profile(self.h, buf, n + 4)))
+        buf = (ctypes.c_ulonglong * (2 * n + 16))()
+        _check(min(0, lib().armour_get_reach_profile(self.h, buf, n + 8)))
         a = np.array(buf[:], dtype=np.uint64)
         return a[:2 * n].reshape(n, 2), a[2 * n:]
 

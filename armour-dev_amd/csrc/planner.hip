@@ -130,8 +130,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
         if ((rc = p->alloc(&p->d_prog, pb.ops.size())) || (rc = p->alloc(&p->d_bytes, 1))) return rc;
         HIPCK(hipMemcpy(p->d_prog, pb.ops.data(), sizeof(Op) * pb.ops.size(), hipMemcpyHostToDevice));
         if (std::getenv("ARMOUR_PROFILE_OPS")) {
-            if ((rc = p->alloc(&p->d_prof, 2 * pb.ops.size() + 8))) return rc;
-            HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 8)));
+            if ((rc = p->alloc(&p->d_prof, 2 * pb.ops.size() + 16))) return rc;
+            HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 16)));
         }
     }
     // reach workspace: two resident workgroups per CU, each with a private arena
@@ -140,7 +140,10 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     ra.prog = p->d_prog;
     ra.nops = p->nops;
     ra.bytes = p->d_bytes;
-    ra.prof = p->d_prof;
+    // ARMOUR_PROFILE_OPS=1: per-op cycles/terms; =2: phase totals (each distorts the other)
+    const char* pm = std::getenv("ARMOUR_PROFILE_OPS");
+    ra.prof = (pm && std::atoi(pm) == 2) ? nullptr : p->d_prof;
+    ra.phase = (pm && std::atoi(pm) == 2) ? p->d_prof + 2 * p->nops : nullptr;
     ra.mode = std::getenv("ARMOUR_ENGINE_MODE") ? std::atoi(std::getenv("ARMOUR_ENGINE_MODE")) : 0;
     ra.dump = nullptr;
     if (std::getenv("ARMOUR_DUMP_OPS")) {
@@ -490,8 +493,8 @@ int armour_get_torque_radius(armour_planner* p, int w, double* radius) {
 int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms, int capacity) {
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (!p->d_prof) return fail(ARMOUR_E_STATE, "op profiling is off (set ARMOUR_PROFILE_OPS before armour_create)");
-    if (cycles_terms && capacity >= p->nops + 4)
-        HIPCK(hipMemcpy(cycles_terms, p->d_prof, sizeof(unsigned long long) * (2 * p->nops + 8), hipMemcpyDeviceToHost));
+    if (cycles_terms && capacity >= p->nops + 8)
+        HIPCK(hipMemcpy(cycles_terms, p->d_prof, sizeof(unsigned long long) * (2 * p->nops + 16), hipMemcpyDeviceToHost));
     return p->nops;
 }
 

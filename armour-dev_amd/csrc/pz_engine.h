@@ -478,19 +478,179 @@ AI void finish_t0(PZH& h, const double* red, const double* abs, int n) {
     UNR for (int e = 0; e < 9; e++) h.absum[e] = e < n ? abs[e] : 0.0;
 }
 
+AI double frob1(double v) { return frob_norm(&v, 1); }
+AI double pick3(const double* m, int i) { return i == 0 ? m[0] : (i == 1 ? m[1] : m[2]); }
+
+// ---------------------------------------------------------------------------------------------
+// group policies: what a simplify makes of an ordered term list. Per term a policy yields up to NV
+// values; per equal-hash group it sums them in term order (the reference's merge) and decides
+// keep / prune; NR reduction slots (a bit mask says which are live); finish() completes the
+// output header from the reduced slots (thread 0).
+
+// plain simplify (PZsparse.cu:284-350): group sum of coefficient blocks, prune by Frobenius norm
+struct PolBlock {
+    static constexpr int NV = 9;
+    static constexpr int NR = 18;   // [0, 9): pruned |sum|, [9, 18): kept |sum| (absum)
+    int n;
+    double thr;
+    AI int nv() const { return n; }
+    AI int nout() const { return n; }
+    AI unsigned mask() const { return ((1u << n) - 1) | (((1u << n) - 1) << 9); }
+    AI void term(const Terms& T, int p, double* v) const { T.coef(p, v); }
+    AI bool group(const double* s, double* out, double* red) const {
+        const bool keep = frob_norm(s, n) > thr;
+        UNR for (int e = 0; e < 9; e++) {
+            if (e < n) {
+                if (keep) { out[e] = s[e]; red[9 + e] = red[9 + e] + fabs(s[e]); }
+                else red[e] = red[e] + fabs(s[e]);
+            }
+        }
+        return keep;
+    }
+    AI void finish(Ctx& x, int o, const double* red) const { finish_t0(x.H[o], red, red + 9, n); }
+};
+
+// fused PZ x PZ cross product of two 3x1 PZs a, b (PZsparse.cu:1118-1167 composes it from element
+// views): six 1x1 products P0 = a1 b2, P1 = a2 b1, P2 = a2 b0, P3 = a0 b2, P4 = a0 b1, P5 = a1 b0,
+// each simplified; r_e = P_2e - P_2e+1, each simplified; stack(r0, r1, r2), simplified. All six
+// products share one term list (T1 a_i, T2 b_j, T3 a_i + b_j), so one ordering serves them all;
+// every intermediate prune is replicated per hash group.
+struct PolCrossPP {
+    static constexpr int NV = 6;
+    static constexpr int NR = 15;   // [0,6) product prunes, [6,9) difference prunes, [9,12) stack prunes, [12,15) absum
+    double thr;
+    const double* ac;               // operand centres (LDS handles)
+    const double* bc;
+    int a, b;                       // operand handle slots
+    AI int nv() const { return 6; }
+    AI int nout() const { return 3; }
+    AI unsigned mask() const { return (1u << NR) - 1; }
+    AI static void prods(const double* u, const double* w, double* v) {
+        v[0] = u[1] * w[2]; v[1] = u[2] * w[1]; v[2] = u[2] * w[0];
+        v[3] = u[0] * w[2]; v[4] = u[0] * w[1]; v[5] = u[1] * w[0];
+    }
+    AI void term(const Terms& T, int p, double* v) const {
+        const int na = T.S[0].cnt, nb = T.S[1].cnt;
+        double u[9], w[9];
+        if (p < na) {
+            T.S[0].read(p, false, u);
+            UNR for (int e = 0; e < 3; e++) w[e] = bc[e];
+        } else if (p < na + nb) {
+            UNR for (int e = 0; e < 3; e++) u[e] = ac[e];
+            T.S[1].read(p - na, false, w);
+        } else {
+            const int q = p - na - nb;
+            T.S[0].read(q / nb, false, u);
+            T.S[1].read(q % nb, false, w);
+        }
+        prods(u, w, v);
+        UNR for (int e = 6; e < 9; e++) v[e] = 0.0;
+    }
+    AI bool group(const double* s, double* out, double* red) const {
+        bool pres[6];
+        UNR for (int p = 0; p < 6; p++) {
+            pres[p] = frob1(s[p]) > thr;
+            if (!pres[p]) red[p] = red[p] + fabs(s[p]);
+        }
+        double vec[3];
+        bool any = false;
+        UNR for (int e = 0; e < 3; e++) {
+            const int P = 2 * e, Q = 2 * e + 1;
+            bool have = pres[P] || pres[Q];
+            const double v = pres[P] ? (pres[Q] ? s[P] + (-s[Q]) : s[P]) : (pres[Q] ? -s[Q] : 0.0);
+            if (have && !(frob1(v) > thr)) { red[6 + e] = red[6 + e] + fabs(v); have = false; }
+            vec[e] = have ? v : 0.0;
+            any = any || have;
+        }
+        if (!any) return false;
+        if (!(frob_norm(vec, 3) > thr)) {
+            UNR for (int e = 0; e < 3; e++) red[9 + e] = red[9 + e] + fabs(vec[e]);
+            return false;
+        }
+        UNR for (int e = 0; e < 3; e++) { out[e] = vec[e]; red[12 + e] = red[12 + e] + fabs(vec[e]); }
+        return true;
+    }
+    // headers of the whole composition: products (PZsparse.cu:944-990 for 1x1 operands), the
+    // differences (:813-834) and the stack (:1087-1116), each plus its own pruned amount
+    AI void finish(Ctx& x, int o, const double* red) const {
+        const PZH& A = x.H[a];
+        const PZH& B = x.H[b];
+        PZH& h = x.H[o];
+        const int ea[6] = {1, 2, 2, 0, 0, 1}, fb[6] = {2, 1, 0, 2, 1, 0};
+        double pc[6], pi[2][6];
+        UNR for (int p = 0; p < 6; p++) {
+            const double ace = pick3(A.center, ea[p]), bcf = pick3(B.center, fb[p]);
+            const double r2 = fabs(ace) + pick3(A.absum, ea[p]);
+            const double r3 = fabs(bcf) + pick3(B.absum, fb[p]);
+            pc[p] = ace * bcf;
+            UNR for (int v = 0; v < 2; v++) {
+                const double ai = pick3(A.ind[v], ea[p]), bi = pick3(B.ind[v], fb[p]);
+                pi[v][p] = ai * bi + (r2 * bi + ai * r3);
+                if (frob1(red[p]) != 0) pi[v][p] = pi[v][p] + red[p];
+            }
+        }
+        double sred[3];
+        UNR for (int e = 0; e < 3; e++) sred[e] = red[9 + e];
+        const bool sadd = frob_norm(sred, 3) != 0;
+        UNR for (int e = 0; e < 3; e++) {
+            h.center[e] = pc[2 * e] - pc[2 * e + 1];
+            UNR for (int v = 0; v < 2; v++) {
+                double iv = pi[v][2 * e] + pi[v][2 * e + 1];
+                if (frob1(red[6 + e]) != 0) iv = iv + red[6 + e];
+                if (sadd) iv = iv + sred[e];
+                h.ind[v][e] = iv;
+            }
+            h.absum[e] = red[12 + e];
+        }
+    }
+};
+
+// deterministic reduction of the masked slots of an NR-block over the group
+AI void block_sum_mask(const Ctx& x, double* v, int nr, unsigned mask) {
+    const Grp& g = x.g;
 #if defined(__HIP_DEVICE_COMPILE__)
-// ---- N <= 64: wave 0 alone, keys and coefficients in registers --------------------------------
-__device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int o, const Terms& T, int N) {
-    const int n = T.nout;
+    UNR for (int e = 0; e < 18; e++) if (e < nr && ((mask >> e) & 1)) v[e] = wsum(v[e]);
+    const int wave = g.tid >> 6, nw = (g.n + 63) >> 6;
+    if ((g.tid & 63) == 0)
+        UNR for (int e = 0; e < 18; e++) if (e < nr && ((mask >> e) & 1)) x.red[wave * 18 + e] = v[e];
+    g.sync();
+    UNR for (int e = 0; e < 18; e++) {
+        if (e < nr && ((mask >> e) & 1)) {
+            double s = x.red[e];
+            for (int w = 1; w < nw; w++) s = s + x.red[w * 18 + e];
+            v[e] = s;
+        }
+    }
+    g.sync();
+#else
+    block_sum(x, v, nr);
+#endif
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// ---- N <= 64: wave 0 alone, keys and term values in registers ---------------------------------
+#define SPHASE(k)                                                                                  \
+    if (x.phase && lane == 0) {                                                                    \
+        const long long c_ = clock64();                                                            \
+        x.phase[k] += (unsigned long long)(c_ - ph_t);                                             \
+        ph_t = c_;                                                                                 \
+    }
+template <class Pol>
+__device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
+    constexpr int NV = Pol::NV;
+    const int nv = pol.nv(), n = pol.nout();
     const int lane = x.g.tid & 63;
+    long long ph_t = x.phase ? clock64() : 0;
     uint64_t h = ~(uint64_t)0;
     double c[9];
     if (lane < N) {
         h = T.hash(lane);
-        T.coef(lane, c);
+        pol.term(T, lane, c);
     } else {
         UNR for (int e = 0; e < 9; e++) c[e] = 0.0;
     }
+    if (x.phase) { UNR for (int e = 0; e < 9; e++) h ^= (c[e] != c[e]) ? 1 : 0; }  // force the loads before the stamp
+    SPHASE(8)
     uint32_t id = (uint32_t)lane;
     int P = 1;
     while (P < N) P <<= 1;
@@ -502,8 +662,9 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
             const bool other_less = key_less(oh, oi, h, id);
             if ((lower == asc) ? other_less : !other_less) { h = oh; id = oi; }
         }
-    // coefficients follow their keys
-    UNR for (int e = 0; e < 9; e++) if (e < n) c[e] = __shfl(c[e], (int)id, 64);
+    SPHASE(9)
+    // term values follow their keys
+    UNR for (int e = 0; e < NV; e++) if (e < nv) c[e] = __shfl(c[e], (int)id, 64);
     const uint64_t prev = __shfl_up(h, 1, 64);
     const bool head = lane < N && (lane == 0 || h != prev);
     const unsigned long long hm = __ballot(head);
@@ -516,26 +677,26 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     UNR for (int e = 0; e < 9; e++) acc[e] = c[e];
     for (int st = 1; st < maxg; st++) {
         double t[9];
-        UNR for (int e = 0; e < 9; e++) if (e < n) t[e] = __shfl(c[e], (lane + st) & 63, 64);
-        if (head && st < size) UNR for (int e = 0; e < 9; e++) if (e < n) acc[e] = acc[e] + t[e];
+        UNR for (int e = 0; e < NV; e++) if (e < nv) t[e] = __shfl(c[e], (lane + st) & 63, 64);
+        if (head && st < size) UNR for (int e = 0; e < NV; e++) if (e < nv) acc[e] = acc[e] + t[e];
     }
-    const bool keep = head && frob_norm(acc, n) > x.thr;
-    double red[9], ab[9];
-    UNR for (int e = 0; e < 9; e++) {
-        red[e] = (head && !keep && e < n) ? fabs(acc[e]) : 0.0;
-        ab[e] = (keep && e < n) ? fabs(acc[e]) : 0.0;
-    }
+    SPHASE(10)
+    double red[Pol::NR], out[9];
+    UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
+    UNR for (int e = 0; e < 9; e++) out[e] = 0.0;
+    const bool keep = head && pol.group(acc, out, red);
+    if (!head) UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
     const unsigned long long km = __ballot(keep);
     const int K = __popcll(km);
     const int pos = __popcll(km & ((1ull << lane) - 1));
     long hoff = 0, coff = 0;
     int ok = 0;
     if (lane == 0) {
-        PZH& out = x.H[o];
-        arena_alloc_t0(x, out, K, n);
-        hoff = out.hoff;
-        coff = out.coff;
-        ok = out.cnt == K;
+        PZH& oh = x.H[o];
+        arena_alloc_t0(x, oh, K, n);
+        hoff = oh.hoff;
+        coff = oh.coff;
+        ok = oh.cnt == K;
         x.A->bytes += T.in_bytes() + (double)K * (8.0 + 8.0 * n);
     }
     hoff = __shfl(hoff, 0, 64);
@@ -544,10 +705,13 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     if (ok && keep) {
         x.A->h[hoff + pos] = h;
         double* dst = x.A->c + coff + (long)pos * n;
-        UNR for (int e = 0; e < 9; e++) if (e < n) dst[e] = acc[e];
+        UNR for (int e = 0; e < 9; e++) if (e < n) dst[e] = out[e];
     }
-    UNR for (int e = 0; e < 9; e++) if (e < n) { red[e] = wsum(red[e]); ab[e] = wsum(ab[e]); }
-    if (lane == 0) finish_t0(x.H[o], red, ab, n);
+    SPHASE(11)
+    const unsigned mask = pol.mask();
+    UNR for (int e = 0; e < Pol::NR; e++) if ((mask >> e) & 1) red[e] = wsum(red[e]);
+    if (lane == 0) pol.finish(x, o, red);
+    SPHASE(12)
 }
 
 // ---- register bitonic: 256 x E keys, E per thread (element index tid * E + r) -----------------
@@ -611,20 +775,22 @@ __device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const 
 #define PHASE(k)                                                                                   \
     if (x.phase && g.tid == 0) {                                                                   \
         const long long c_ = clock64();                                                            \
-        atomicAdd(&x.phase[k], (unsigned long long)(c_ - ph_t));                                   \
+        x.phase[k] += (unsigned long long)(c_ - ph_t);                                             \
         ph_t = c_;                                                                                 \
     }
 #else
 #define PHASE(k)
 #endif
 
-// ---- N > 64: whole group. Header of o set and sources staged (caller's barrier done). ---------
-AI void simplify_big(Ctx& x, int o, const Terms& T, int N) {
+// ---- N > 64: whole group. Output header initialised and sources staged (caller's barrier done).
+template <class Pol>
+AI void simplify_big(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
     const Grp& g = x.g;
 #if defined(__HIP_DEVICE_COMPILE__)
     long long ph_t = x.phase ? clock64() : 0;
 #endif
-    const int n = T.nout;
+    constexpr int NV = Pol::NV;
+    const int nv = pol.nv(), n = pol.nout();
     uint64_t* kh = x.kh;
     uint32_t* ki = x.ki;
     int* kp = x.kp;
@@ -673,23 +839,20 @@ AI void simplify_big(Ctx& x, int o, const Terms& T, int N) {
     }
     g.sync();
     PHASE(1)
-    // group sums in term order, keep flags
-    double red[9], acc[9], tmp[9];
-    UNR for (int e = 0; e < 9; e++) red[e] = 0.0;
+    // group sums in term order, keep flags, pruned amounts
+    double red[Pol::NR], acc[9], tmp[9], out[9];
+    UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
+    UNR for (int e = 0; e < 9; e++) out[e] = 0.0;
     for (int q = g.tid; q < N; q += g.n) {
         const bool head = q == 0 || kh[q] != kh[q - 1];
         int keep = 0;
         if (head) {
-            T.coef(ki[q], acc);
+            pol.term(T, ki[q], acc);
             for (int r = q + 1; r < N && kh[r] == kh[q]; r++) {
-                T.coef(ki[r], tmp);
-                UNR for (int e = 0; e < 9; e++) acc[e] = acc[e] + tmp[e];
+                pol.term(T, ki[r], tmp);
+                UNR for (int e = 0; e < NV; e++) if (e < nv) acc[e] = acc[e] + tmp[e];
             }
-            if (frob_norm(acc, n) <= x.thr) {
-                UNR for (int e = 0; e < 9; e++) red[e] = red[e] + fabs(acc[e]);
-            } else {
-                keep = 1;
-            }
+            keep = pol.group(acc, out, red) ? 1 : 0;
         }
         kp[q] = keep;
     }
@@ -703,31 +866,168 @@ AI void simplify_big(Ctx& x, int o, const Terms& T, int N) {
     g.sync();
     PHASE(3)
     const long hoff = x.H[o].hoff, coff = x.H[o].coff;
-    double ab[9];
-    UNR for (int e = 0; e < 9; e++) ab[e] = 0.0;
     if (x.H[o].cnt == K) {
+        double dummy[Pol::NR];
         for (int q = g.tid; q < N; q += g.n) {
             const bool head = q == 0 || kh[q] != kh[q - 1];
             if (!head) continue;
             const bool keep = (q + 1 < N) ? (kp[q + 1] != kp[q]) : (kp[q] != K);
             if (!keep) continue;
-            T.coef(ki[q], acc);
+            pol.term(T, ki[q], acc);
             for (int r = q + 1; r < N && kh[r] == kh[q]; r++) {
-                T.coef(ki[r], tmp);
-                UNR for (int e = 0; e < 9; e++) acc[e] = acc[e] + tmp[e];
+                pol.term(T, ki[r], tmp);
+                UNR for (int e = 0; e < NV; e++) if (e < nv) acc[e] = acc[e] + tmp[e];
             }
+            UNR for (int e = 0; e < Pol::NR; e++) dummy[e] = 0.0;
+            pol.group(acc, out, dummy);
             const long pos = kp[q];
             x.A->h[hoff + pos] = kh[q];
             double* dst = x.A->c + coff + pos * n;
-            UNR for (int e = 0; e < 9; e++) if (e < n) { dst[e] = acc[e]; ab[e] = ab[e] + fabs(acc[e]); }
+            UNR for (int e = 0; e < 9; e++) if (e < n) dst[e] = out[e];
         }
     }
     PHASE(4)
-    double v[18];
-    UNR for (int e = 0; e < 9; e++) { v[e] = red[e]; v[9 + e] = ab[e]; }
-    block_sum(x, v, 18);
+    block_sum_mask(x, red, Pol::NR, pol.mask());
     PHASE(5)
-    if (g.tid == 0) finish_t0(x.H[o], v, v + 9, n);
+    if (g.tid == 0) pol.finish(x, o, red);
+}
+
+// ---- fused PZ x constant / constant x PZ cross products (PZsparse.cu:1118-1167) -----------------
+// r_e = sA_e * a[iA_e] - sB_e * a[iB_e] (two scaled element views of the 3x1 source, subtracted,
+// simplified), then stack(r0, r1, r2) simplified. The source's monomials map one to one (its hash
+// order is kept), so no ordering is needed.
+struct CrossC {
+    int iA[3], iB[3];
+    double sA[3], sB[3];
+};
+// kind 0: a x v (PZ x const), kind 1: v x a (const x PZ), as the reference's two overloads
+AI CrossC cross_const_table(int kind, const double* v) {
+    CrossC C;
+    if (kind == 0) {
+        C.iA[0] = 1; C.sA[0] = v[2]; C.iB[0] = 2; C.sB[0] = v[1];
+        C.iA[1] = 2; C.sA[1] = v[0]; C.iB[1] = 0; C.sB[1] = v[2];
+        C.iA[2] = 0; C.sA[2] = v[1]; C.iB[2] = 1; C.sB[2] = v[0];
+    } else {
+        C.iA[0] = 2; C.sA[0] = v[1]; C.iB[0] = 1; C.sB[0] = v[2];
+        C.iA[1] = 0; C.sA[1] = v[2]; C.iB[1] = 2; C.sB[1] = v[0];
+        C.iA[2] = 1; C.sA[2] = v[0]; C.iB[2] = 0; C.sB[2] = v[1];
+    }
+    return C;
+}
+// one source monomial m -> output row; red: [0,3) difference prunes, [3,6) stack prunes, [6,9) absum
+AI bool cross_const_mono(const CrossC& C, const double* m, double thr, double* out, double* red) {
+    double vec[3];
+    bool any = false;
+    UNR for (int e = 0; e < 3; e++) {
+        const double xa = C.sA[e] * pick3(m, C.iA[e]);
+        const double xb = -(C.sB[e] * pick3(m, C.iB[e]));
+        const double v = xa + xb;
+        bool have = true;
+        if (!(frob1(v) > thr)) { red[e] = red[e] + fabs(v); have = false; }
+        vec[e] = have ? v : 0.0;
+        any = any || have;
+    }
+    if (!any) return false;
+    if (!(frob_norm(vec, 3) > thr)) {
+        UNR for (int e = 0; e < 3; e++) red[3 + e] = red[3 + e] + fabs(vec[e]);
+        return false;
+    }
+    UNR for (int e = 0; e < 3; e++) { out[e] = vec[e]; red[6 + e] = red[6 + e] + fabs(vec[e]); }
+    return true;
+}
+// header: views (t0_view), differences (PZsparse.cu:813-834), stack, each plus its pruned amount
+AI void cross_const_finish(PZH& h, const PZH& A, const CrossC& C, const double* red) {
+    double sred[3];
+    UNR for (int e = 0; e < 3; e++) sred[e] = red[3 + e];
+    const bool sadd = frob_norm(sred, 3) != 0;
+    UNR for (int e = 0; e < 3; e++) {
+        h.center[e] = pick3(A.center, C.iA[e]) * C.sA[e] - pick3(A.center, C.iB[e]) * C.sB[e];
+        UNR for (int v = 0; v < 2; v++) {
+            double iv = pick3(A.ind[v], C.iA[e]) * fabs(C.sA[e]) + pick3(A.ind[v], C.iB[e]) * fabs(C.sB[e]);
+            if (frob1(red[e]) != 0) iv = iv + red[e];
+            if (sadd) iv = iv + sred[e];
+            h.ind[v][e] = iv;
+        }
+        h.absum[e] = red[6 + e];
+    }
+}
+
+// the whole op; the header of o (3x1) is initialised by the caller's thread 0; ends without barrier
+AI void cross_const(Ctx& x, int o, int a, const CrossC& C) {
+    const Grp& g = x.g;
+    const PZH& A = x.H[a];
+    const int N = A.cnt;
+    const Src S = src_of(x, A);
+    double red[9], out[9], m[9];
+    UNR for (int e = 0; e < 9; e++) { red[e] = 0.0; out[e] = 0.0; }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (N <= 64) {
+        if (g.tid >= 64) return;
+        const int lane = g.tid;
+        bool keep = false;
+        if (lane < N) {
+            S.read(lane, false, m);
+            keep = cross_const_mono(C, m, x.thr, out, red);
+        }
+        const unsigned long long km = __ballot(keep);
+        const int K = __popcll(km);
+        const int pos = __popcll(km & ((1ull << lane) - 1));
+        long hoff = 0, coff = 0;
+        int ok = 0;
+        if (lane == 0) {
+            PZH& oh = x.H[o];
+            arena_alloc_t0(x, oh, K, 3);
+            hoff = oh.hoff;
+            coff = oh.coff;
+            ok = oh.cnt == K;
+            x.A->bytes += (double)N * 32.0 + (double)K * 32.0;
+        }
+        hoff = __shfl(hoff, 0, 64);
+        coff = __shfl(coff, 0, 64);
+        ok = __shfl(ok, 0, 64);
+        if (ok && keep) {
+            x.A->h[hoff + pos] = S.h[lane];
+            double* dst = x.A->c + coff + (long)pos * 3;
+            UNR for (int e = 0; e < 3; e++) dst[e] = out[e];
+        }
+        UNR for (int e = 0; e < 9; e++) red[e] = wsum(red[e]);
+        if (lane == 0) cross_const_finish(x.H[o], A, C, red);
+        return;
+    }
+#endif
+    int* kp = N <= x.cap_lds ? x.kp : x.gkp;
+    if (N > x.cap_lds && N > x.cap_glb) {
+        if (g.tid == 0) { *x.err |= ERR_SORTCAP; x.H[o].cnt = 0; }
+        return;
+    }
+    for (int k = g.tid; k < N; k += g.n) {
+        S.read(k, false, m);
+        kp[k] = cross_const_mono(C, m, x.thr, out, red) ? 1 : 0;
+    }
+    g.sync();
+    const int K = block_scan(x, kp, N);
+    if (g.tid == 0) {
+        arena_alloc_t0(x, x.H[o], K, 3);
+        x.A->bytes += (double)N * 32.0 + (double)K * 32.0;
+    }
+    g.sync();
+    const long hoff = x.H[o].hoff, coff = x.H[o].coff;
+    if (x.H[o].cnt == K) {
+        double dummy[9];
+        for (int k = g.tid; k < N; k += g.n) {
+            const bool keep = (k + 1 < N) ? (kp[k + 1] != kp[k]) : (kp[k] != K);
+            if (!keep) continue;
+            S.read(k, false, m);
+            UNR for (int e = 0; e < 9; e++) dummy[e] = 0.0;
+            cross_const_mono(C, m, x.thr, out, dummy);
+            const long pos = kp[k];
+            x.A->h[hoff + pos] = S.h[k];
+            double* dst = x.A->c + coff + pos * 3;
+            UNR for (int e = 0; e < 3; e++) dst[e] = out[e];
+        }
+    }
+    block_sum_mask(x, red, 9, 0x1ff);
+    if (g.tid == 0) cross_const_finish(x.H[o], A, C, red);
 }
 
 AI void hdr_init(PZH& h, int R, int C) {
@@ -812,6 +1112,19 @@ AI void header_mul(Ctx& x, int o, int a, int b, const Terms& T) {
     }
     if (as && !bs && B.R != 1 && A.cnt > 0 && B.cnt > 0) *x.err |= ERR_HANDLES;  // Eigen assert in the reference
     if (!as && !bs && !(A.R == 3 && A.C == 3 && B.R == 3)) *x.err |= ERR_HANDLES;  // block shape outside matmul()
+}
+
+// fused PZ x PZ cross: the term list of the six 1x1 products is the product term list of the two
+// full 3x1 operands (hashes only; PolCrossPP evaluates the coefficients)
+AI void terms_cross_pp(const Ctx& x, int a, int b, Terms& T) {
+    const PZH& A = x.H[a];
+    const PZH& B = x.H[b];
+    T.kind = 0; T.ns = 2;
+    T.places = 0; T.negs = 0;
+    T.S[0] = src_of(x, A); T.S[1] = src_of(x, B);
+    T.Ac = A.center; T.Bc = B.center;
+    T.AR = 3; T.AC = 1; T.BC = 1;
+    T.nout = 3;
 }
 
 // stack three 1x1 PZs into a 3x1 (PZsparse.cu:1087-1116)

@@ -173,8 +173,12 @@ __host__ __device__ __attribute__((noinline)) JrsJoint jrs_joint(const RobotPara
 
 enum : int {
     OP_JRS, OP_MAKE1D, OP_MAKEROT, OP_MAKEBOX, OP_CONST, OP_ZERO, OP_VIEW, OP_TRANSPOSE,
-    OP_MUL, OP_ADD, OP_STACK3, OP_ADD1D, OP_EMIT_LINK, OP_EMIT_TORQUE, OP_TORQUE_RADIUS, OP_NCODES
+    OP_MUL, OP_ADD, OP_STACK3, OP_ADD1D, OP_EMIT_LINK, OP_EMIT_TORQUE, OP_TORQUE_RADIUS,
+    OP_CROSS_C,   // fused cross with a constant vector: o, a = PZ, b = vector table (0 trans, 1 com), c = row, i = 0: a x v, 1: v x a
+    OP_CROSS_PP,  // fused PZ x PZ cross: o, a, b
+    OP_NCODES
 };
+constexpr int VEC_TRANS = 0, VEC_COM = 1;
 enum : int { CONST_RPY = 0, CONST_TRANS = 1, CONST_MASS = 2, CONST_INERTIA = 3 };
 
 struct Op {
@@ -432,7 +436,8 @@ T0FN void t0_torque_radius(const RobotParams& rp, const ReachOut& out, long j, c
 AI int op_terms(const Ctx& x, const Op& op) {
     const PZH& A = x.H[op.a];
     const PZH& B = x.H[op.b];
-    if (op.code == OP_MUL) return A.cnt + B.cnt + A.cnt * B.cnt;
+    if (op.code == OP_CROSS_C) return A.cnt;
+    if (op.code == OP_MUL || op.code == OP_CROSS_PP) return A.cnt + B.cnt + A.cnt * B.cnt;
     if (op.code == OP_STACK3) return A.cnt + B.cnt + x.H[op.c].cnt;
     return A.cnt + B.cnt;
 }
@@ -466,11 +471,18 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
     const int tid = x.g.tid;
     double* rdist = scratch;
     double* ured = scratch + NF;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const bool stamp = (prof || x.phase) && tid == 0;
+    long long c_end = stamp ? clock64() : 0;
+#endif
     for (int pc = 0; pc < nops; pc++) {
         const Op op = prog[pc];
 #if defined(__HIP_DEVICE_COMPILE__)
         long long c0 = 0;
-        if (prof && tid == 0) c0 = clock64();
+        if (stamp) {
+            c0 = clock64();
+            if (x.phase) x.phase[13] += (unsigned long long)(c0 - c_end);  // between ops
+        }
 #endif
         switch (op.code) {
             case OP_JRS:
@@ -498,15 +510,53 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
             case OP_EMIT_LINK: if (tid == 0) t0_emit_link(x, out, j, op.a, op.i); break;
             case OP_EMIT_TORQUE: if (tid == 0) t0_emit_torque(x, out, j, op.a, op.i, rdist, ured); break;
             case OP_TORQUE_RADIUS: if (tid == 0) t0_torque_radius(rp, out, j, rdist, ured); break;
+            case OP_CROSS_C: {
+                const double* v = op.b == VEC_TRANS ? &rp.trans[3 * op.c] : &rp.com[3 * op.c];
+                const CrossC C = cross_const_table(op.i, v);
+                if (tid == 0) hdr_init(x.H[op.o], 3, 1);
+                cross_const(x, op.o, op.a, C);
+                break;
+            }
+            case OP_CROSS_PP: {
+                Terms Tm;
+                terms_cross_pp(x, op.a, op.b, Tm);
+                const int N = op_terms(x, op);
+                PolCrossPP pol;
+                pol.thr = x.thr;
+                pol.ac = x.H[op.a].center;
+                pol.bc = x.H[op.b].center;
+                pol.a = op.a;
+                pol.b = op.b;
+                if (tid == 0) hdr_init(x.H[op.o], 3, 1);
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (N <= 64 && !(x.mode & 1)) {
+                    if (tid < 64) simplify_small(x, op.o, Tm, pol, N);
+                    break;
+                }
+#endif
+                stage_sources(x, Tm);
+                x.g.sync();
+                simplify_big(x, op.o, Tm, pol, N);
+                break;
+            }
             default: {
                 // MUL / ADD / STACK3 / ADD1D: term list, header, simplify
                 Terms Tm;
                 op_terms_of(x, op, Tm);
                 const int N = op_terms(x, op);
+#if defined(__HIP_DEVICE_COMPILE__)
+                long long ph0 = (x.phase && tid == 0) ? clock64() : 0;
+#endif
                 if (tid == 0) op_header(x, op, Tm);
 #if defined(__HIP_DEVICE_COMPILE__)
+                if (x.phase && tid == 0) x.phase[14] += (unsigned long long)(clock64() - ph0);
+#endif
+                PolBlock pol;
+                pol.n = Tm.nout;
+                pol.thr = x.thr;
+#if defined(__HIP_DEVICE_COMPILE__)
                 if (N <= 64 && !(x.mode & 1)) {
-                    if (tid < 64) simplify_small(x, op.o, Tm, N);
+                    if (tid < 64) simplify_small(x, op.o, Tm, pol, N);
                     break;
                 }
                 long long pt = (x.phase && tid == 0) ? clock64() : 0;
@@ -514,9 +564,9 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                 stage_sources(x, Tm);
                 x.g.sync();
 #if defined(__HIP_DEVICE_COMPILE__)
-                if (x.phase && tid == 0) atomicAdd(&x.phase[6], (unsigned long long)(clock64() - pt));
+                if (x.phase && tid == 0) x.phase[6] += (unsigned long long)(clock64() - pt);
 #endif
-                simplify_big(x, op.o, Tm, N);
+                simplify_big(x, op.o, Tm, pol, N);
                 break;
             }
         }
@@ -532,9 +582,14 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
             x.g.sync();
         }
 #if defined(__HIP_DEVICE_COMPILE__)
-        if (prof && tid == 0) {
-            atomicAdd(&prof[2 * pc], (unsigned long long)(clock64() - c0));
-            if (op.code >= OP_MUL && op.code <= OP_ADD1D) atomicAdd(&prof[2 * pc + 1], (unsigned long long)op_terms(x, op));
+        if (stamp) {
+            c_end = clock64();
+            if (prof) {
+                atomicAdd(&prof[2 * pc], (unsigned long long)(c_end - c0));
+                if ((op.code >= OP_MUL && op.code <= OP_ADD1D) || op.code >= OP_CROSS_C)
+                    atomicAdd(&prof[2 * pc + 1], (unsigned long long)op_terms(x, op));
+                c_end = clock64();
+            }
         }
 #endif
     }
@@ -573,8 +628,15 @@ struct ProgramBuilder {
     int cnst(int kind, int i) { return out(OP_CONST, kind, 0, 0, i); }
     int zero(int R, int C, int gravity = 0) { return out(OP_ZERO, 0, R, C, gravity); }
 
-    // cross products (PZsparse.cu:1118-1167), component by component as the reference does
-    int cross_pm(int a, const double* b) {  // PZ x const
+    // cross products (PZsparse.cu:1118-1167). fused = true: one op each (OP_CROSS_C / OP_CROSS_PP,
+    // every intermediate simplify replicated inside); false: composed from element views, products,
+    // differences and a stack, op by op as the reference composes them (kept for A/B checks)
+    bool fused = true;
+    const RobotParams* rp = nullptr;
+    const double* vec(int src, int row) const { return src == VEC_TRANS ? &rp->trans[3 * row] : &rp->com[3 * row]; }
+    int cross_pm(int a, int src, int row) {  // PZ x const
+        if (fused) return out(OP_CROSS_C, a, src, row, 0);
+        const double* b = vec(src, row);
         const int s0 = scaled_elem(a, 1, b[2]), s1 = scaled_elem(a, 2, b[1]);
         const int r0 = sub(s0, s1);
         rel({s0, s1});
@@ -588,7 +650,9 @@ struct ProgramBuilder {
         rel({r0, r1, r2});
         return o;
     }
-    int cross_mp(const double* a, int b) {  // const x PZ
+    int cross_mp(int src, int row, int b) {  // const x PZ
+        if (fused) return out(OP_CROSS_C, b, src, row, 1);
+        const double* a = vec(src, row);
         const int s0 = scaled_elem(b, 2, a[1]), s1 = scaled_elem(b, 1, a[2]);
         const int r0 = sub(s0, s1);
         rel({s0, s1});
@@ -603,6 +667,7 @@ struct ProgramBuilder {
         return o;
     }
     int cross_pp(int a, int b) {  // PZ x PZ
+        if (fused) return out(OP_CROSS_PP, a, b);
         const int a0 = elem(a, 0), a1 = elem(a, 1), a2 = elem(a, 2);
         const int b0 = elem(b, 0), b1 = elem(b, 1), b2 = elem(b, 2);
         int p = mul(a1, b2), q = mul(a2, b1);
@@ -621,6 +686,7 @@ struct ProgramBuilder {
 
     // the whole job, op for op KPR/Trajectory.cu:63-254, Dynamics.cu:69-181, armour_main.cu:118-211
     void build(const RobotParams& rp) {
+        this->rp = &rp;
         const int NJ = rp.num_joints;
         int R[MAX_J + 1], RT[MAX_J], QD[NF], QDA[NF], QDD[NF];
         emit(OP_JRS);
@@ -669,13 +735,11 @@ struct ProgramBuilder {
         int W = zero(3, 1), WDOT = zero(3, 1), WAUX = zero(3, 1), LIN = zero(3, 1, 1);
         int F[MAX_J], N[MAX_J];
         for (int i = 0; i < NJ; i++) {
-            const double* p = &rp.trans[3 * i];
-            const double* c = &rp.com[3 * i];
             // line 16
             {
-                const int t1 = cross_pm(WDOT, p);
+                const int t1 = cross_pm(WDOT, VEC_TRANS, i);
                 const int t2 = add(LIN, t1);
-                const int t3 = cross_pm(WAUX, p);
+                const int t3 = cross_pm(WAUX, VEC_TRANS, i);
                 const int t4 = cross_pp(W, t3);
                 const int t5 = add(t2, t4);
                 const int lin = mul(RT[i], t5);
@@ -719,9 +783,9 @@ struct ProgramBuilder {
             }
             // line 23 & 27
             {
-                const int t1 = cross_pm(WDOT, c);
+                const int t1 = cross_pm(WDOT, VEC_COM, i);
                 const int t2 = add(LIN, t1);
-                const int t3 = cross_pm(WAUX, c);
+                const int t3 = cross_pm(WAUX, VEC_COM, i);
                 const int t4 = cross_pp(W, t3);
                 const int t5 = add(t2, t4);
                 const int m = cnst(CONST_MASS, i);
@@ -744,10 +808,10 @@ struct ProgramBuilder {
             // line 29: n = N + R*n + cross(com, F) + cross(p_{i+1}, R*f); R*f evaluated once
             const int t1 = mul(R[i + 1], NN);
             const int t2 = add(N[i], t1);
-            const int t3 = cross_mp(&rp.com[3 * i], F[i]);
+            const int t3 = cross_mp(VEC_COM, i, F[i]);
             const int t4 = add(t2, t3);
             const int t5 = mul(R[i + 1], FF);
-            const int t6 = cross_mp(&rp.trans[3 * (i + 1)], t5);
+            const int t6 = cross_mp(VEC_TRANS, i + 1, t5);
             const int nn = add(t4, t6);
             rel({t1, t2, t3, t4, t6, NN});
             NN = nn;

@@ -28,6 +28,7 @@ struct ReachArgs {
     unsigned long long* bytes;  // algorithmic monomial bytes of all jobs (one atomic per job)
     unsigned long long* prof;   // optional per-op [cycles, terms] (null: off)
     int mode;                   // engine diagnostics (Ctx::mode)
+    unsigned long long* phase;  // optional phase cycle totals [16] (null: off; exclusive with prof)
     double* dump;               // optional op-by-op state of job 0 (null: off)
 };
 
@@ -44,6 +45,7 @@ __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotPara
     __shared__ JrsJoint jrs[NF];
     __shared__ double scratch[2 * NF];
     __shared__ double q0s[NF], qd0s[NF], qdd0s[NF];
+    __shared__ unsigned long long phase_acc[16];
 
     const RobotParams& rp = *rpp;
     Ctx x;
@@ -61,7 +63,8 @@ __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotPara
     x.iscan = iscan;
     x.err = &err;
     x.thr = rp.simplify_threshold;
-    x.phase = a.prof ? a.prof + 2 * a.nops : nullptr;
+    x.phase = a.phase ? phase_acc : nullptr;
+    if (threadIdx.x < 16) phase_acc[threadIdx.x] = 0;
     x.mode = a.mode;
 
     const long njobs = (long)a.W * a.T;
@@ -88,6 +91,10 @@ __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotPara
         if (threadIdx.x == 0) {
             if (err) atomicOr(&out.err[w], err);
             atomicAdd(a.bytes, (unsigned long long)arena.bytes);
+        }
+        if (a.phase && threadIdx.x < 16) {
+            atomicAdd(&a.phase[threadIdx.x], phase_acc[threadIdx.x]);
+            phase_acc[threadIdx.x] = 0;
         }
         __syncthreads();
     }

@@ -60,16 +60,26 @@ def cpu_baseline(worlds, T, seconds):
                 sample=f"{done} full plans (oracle C++ restatement, T={T}, O={len(worlds[0][4])}) in {dt:.1f}s")
 
 
+def lib_digest():
+    import hashlib
+
+    from armour_amd import LIB_PATH
+
+    return hashlib.sha1(open(LIB_PATH, "rb").read()).hexdigest()[:16]
+
+
 def traffic_record(T, O, batch):
     """HBM traffic per reach_kernel launch from the newest committed PMC summary of the same
-    workload (profiles/r*_reach_traffic.json, made by tools/gpu_prof.sh + tools/pmc_traffic.py:
-    separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected); None if there is none."""
+    workload AND the same library build (profiles/r*_reach_traffic.json, made by tools/gpu_prof.sh
+    + tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected); None if
+    there is none."""
     import glob
 
     best = None
+    digest = lib_digest()
     for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_reach_traffic.json"))):
         rec = json.load(open(fn))
-        if rec.get("config") == dict(T=T, O=O, batch=batch):
+        if rec.get("config") == dict(T=T, O=O, batch=batch) and rec.get("lib_sha1") == digest:
             best = (fn, rec)
     return best
 

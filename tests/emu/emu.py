@@ -21,8 +21,10 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def reach_job(world, T, t):
-    """Outputs of job (world, t) as the kernel writes them."""
+def reach_job(world, T, t, fused=True):
+    """Outputs of job (world, t) as the kernel writes them (fused: the program's cross products
+    as single ops, else composed from views / products / differences / stack)."""
+    lib().emu_set_unfused(0 if fused else 1)
     q0, qd0, qdd0 = [np.ascontiguousarray(np.asarray(a, dtype=np.float64)) for a in world[:3]]
     o = dict(link_gens=np.zeros((NJ, 18)), link_center=np.zeros((NJ, 3)), link_rad=np.zeros((NJ, 3)),
              link_cnt=np.zeros(NJ, np.int32), link_hash=np.zeros((NJ, CAP_LM), np.uint16),

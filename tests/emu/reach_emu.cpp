@@ -10,7 +10,9 @@
 using namespace armour;
 
 static double* g_dump = nullptr;
+static int g_unfused = 0;
 extern "C" void emu_set_dump(double* d) { g_dump = d; }
+extern "C" void emu_set_unfused(int u) { g_unfused = u; }
 extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, const double* qdd0,
                          double* link_gens, double* link_center, double* link_rad, int* link_cnt,
                          uint16_t* link_hash, double* link_coef, double* tq_center, double* tq_rad,
@@ -19,8 +21,12 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     static RobotParams rp;
     static bool init = false;
     if (!init) { kinova_gen3(rp); init = true; }
-    static ProgramBuilder pb;
-    if (pb.ops.empty()) pb.build(rp);
+    static ProgramBuilder pbf, pbu;  // fused / composed cross products
+    ProgramBuilder& pb = g_unfused ? pbu : pbf;
+    if (pb.ops.empty()) {
+        pb.fused = !g_unfused;
+        pb.build(rp);
+    }
     const long cap = 1 << 22;
     std::vector<uint64_t> ah(cap);
     std::vector<double> ac(cap * 3);

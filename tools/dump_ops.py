@@ -28,7 +28,7 @@ else:
     L.emu_reach(100, 0, *[a.ctypes.data_as(ctypes.c_void_p) for a in (q0, qd0, qdd0)], *[b.ctypes.data_as(ctypes.c_void_p) for b in bufs],
                 ctypes.byref(used), ctypes.byref(bts), ctypes.byref(nops), ctypes.byref(nsl))
     g = np.load(os.path.join(out, 'dump_gpu.npy'))
-    names = ['JRS', 'MAKE1D', 'MAKEROT', 'MAKEBOX', 'CONST', 'ZERO', 'VIEW', 'TRANSPOSE', 'MUL', 'ADD', 'STACK3', 'ADD1D', 'EMIT_LINK', 'EMIT_TORQUE', 'TORQUE_RADIUS']
+    names = ['JRS', 'MAKE1D', 'MAKEROT', 'MAKEBOX', 'CONST', 'ZERO', 'VIEW', 'TRANSPOSE', 'MUL', 'ADD', 'STACK3', 'ADD1D', 'EMIT_LINK', 'EMIT_TORQUE', 'TORQUE_RADIUS', 'CROSS_C', 'CROSS_PP']
     bad = np.where(np.abs(g - d).max(1) > 1e-12 * (1 + np.abs(d).max(1)))[0]
     print('diverging ops:', len(bad))
     for k in bad[:12]:

@@ -31,15 +31,23 @@ for W in [8, 64]:
     t0 = time.time(); res, tm = P.plan(ws); dt = time.time() - t0
     print(f'W={W}: {dt*1e3:.1f} ms wall, {W/dt:.1f} plans/s, timing {tm}, feasible {sum(r["feasible"] for r in res)}/{W}, iters {[r["iterations"] for r in res[:8]]}', flush=True)
 # per-op profile of the reach program (one reach of 64 worlds)
-if os.environ.get('ARMOUR_PROFILE_OPS'):
+if os.environ.get('ARMOUR_PROFILE_OPS') == '2':
+    P2 = A.Planner(T=T, max_obstacles=O, max_worlds=64)
+    ws = [A.make_world(100 + s, O) for s in range(64)]
+    tm = P2.reach(ws)
+    prof, phase = P2.reach_profile()
+    ph = (phase.astype(np.float64) / (64 * T)).round(0)
+    print('reach', tm)
+    print('big-path phases cycles/job [-, order, pass1, scan+alloc, pass2, blocksum, stage, -]:', ph[:8])
+    print('small-path phases cycles/job [load, sort, groups, keep+write, reduce+finish]:', ph[8:13], 'between ops', ph[13], 'headers', ph[14])
+elif os.environ.get('ARMOUR_PROFILE_OPS'):
     names = ['JRS', 'MAKE1D', 'MAKEROT', 'MAKEBOX', 'CONST', 'ZERO', 'VIEW', 'TRANSPOSE', 'MUL', 'ADD', 'STACK3', 'ADD1D',
-             'EMIT_LINK', 'EMIT_TORQUE', 'TORQUE_RADIUS']
+             'EMIT_LINK', 'EMIT_TORQUE', 'TORQUE_RADIUS', 'CROSS_C', 'CROSS_PP']
     P2 = A.Planner(T=T, max_obstacles=O, max_worlds=64)
     ws = [A.make_world(100 + s, O) for s in range(64)]
     P2.reach(ws)
     prof, phase = P2.reach_profile()
     prof = prof.astype(np.float64)
-    print('big-path phases cycles/job [keys, sort, pass1, scan+alloc, pass2, blocksum, -, prep]:', (phase.astype(np.float64) / (64 * T)).round(0))
     codes = P2.reach_program()
     jobs = 64 * T
     tot = prof[:, 0].sum()
@@ -50,7 +58,7 @@ if os.environ.get('ARMOUR_PROFILE_OPS'):
             print(f'  {names[c]:14s} n={m.sum():4d} cycles/job {prof[m, 0].sum() / jobs:10.0f} ({100 * prof[m, 0].sum() / tot:5.1f}%) terms/job {prof[m, 1].sum() / jobs:9.0f}')
     terms = prof[:, 1] / jobs
     for lo, hi in [(0, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 1 << 30)]:
-        m = (codes >= 8) & (codes <= 11) & (terms > lo) & (terms <= hi)
+        m = (((codes >= 8) & (codes <= 11)) | (codes >= 15)) & (terms > lo) & (terms <= hi)
         print(f'  terms in ({lo},{hi}]: ops {m.sum():4d} cycles/job {prof[m, 0].sum() / jobs:10.0f} terms/job {prof[m, 1].sum() / jobs:9.0f}')
     order = np.argsort(-prof[:, 0])[:10]
     for k in order:
