@@ -15,16 +15,15 @@ namespace armour {
 // helpers
 __device__ inline double ipow(double x, int d) { return d == 0 ? 1.0 : d == 1 ? x : d == 2 ? x * x : x * x * x; }
 
-__device__ inline double wave_sum(double v) {
-    for (int m = 32; m > 0; m >>= 1) v = v + __shfl_xor(v, m, 64);
-    return v;
-}
+// wave_sum (wave.h): DPP / permlane butterfly
 __device__ inline double wave_max(double v) {
-    for (int m = 32; m > 0; m >>= 1) v = fmax(v, __shfl_xor(v, m, 64));
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = fmax(v, xor_f64(v, m));
     return v;
 }
 __device__ inline double wave_min(double v) {
-    for (int m = 32; m > 0; m >>= 1) v = fmin(v, __shfl_xor(v, m, 64));
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = fmin(v, xor_f64(v, m));
     return v;
 }
 // kind: 0 sum, 1 max, 2 min; result written by thread 0 to out
@@ -334,9 +333,10 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
                 if (neg > best) { best = neg; seq = 2 * lane + 1; }
             }
         }
-        for (int m = 32; m > 0; m >>= 1) {
-            const double ob = __shfl_xor(best, m, 64);
-            const int os = __shfl_xor(seq, m, 64);
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) {
+            const double ob = xor_f64(best, m);
+            const int os = xor_i32(seq, m);
             if (ob > best || (ob == best && os < seq)) { best = ob; seq = os; }
         }
         const int id = seq < (1 << 30) ? (seq >> 1) : 0;

@@ -30,6 +30,7 @@
 // The group abstraction (Grp) lets the same code run as a sequential host emulation in tests.
 #pragma once
 #include "common.h"
+#include "wave.h"
 
 #define AI __host__ __device__ inline __attribute__((always_inline))
 #define UNR _Pragma("unroll")
@@ -136,9 +137,11 @@ AI uint64_t mono_hash(const Ctx& x, const PZH& h, int k) { return x.A->h[h.hoff 
 // ---------------------------------------------------------------------------------------------
 // wave / block primitives
 #if defined(__HIP_DEVICE_COMPILE__)
-__device__ inline __attribute__((always_inline)) double wsum(double v) {
-    UNR for (int m = 32; m > 0; m >>= 1) v = v + __shfl_xor(v, m, 64);
-    return v;
+__device__ inline __attribute__((always_inline)) double wsum(double v) { return wave_sum(v); }
+__device__ inline __attribute__((always_inline)) long bcast0(long v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 0);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), 0);
+    return (long)(((uint64_t)hi << 32) | lo);
 }
 #endif
 
@@ -181,11 +184,7 @@ AI int block_scan(const Ctx& x, int* kp, int N) {
     for (int i = lo; i < hi; i++) s += kp[i];
 #if defined(__HIP_DEVICE_COMPILE__)
     const int lane = g.tid & 63, wave = g.tid >> 6, nw = (g.n + 63) >> 6;
-    int inc = s;
-    UNR for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += y;
-    }
+    const int inc = wave_incl_scan(s);
     if (lane == 63) x.iscan[wave] = inc;
     g.sync();
     int base = 0, total = 0;
@@ -654,30 +653,33 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     uint32_t id = (uint32_t)lane;
     int P = 1;
     while (P < N) P <<= 1;
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t oh = __shfl_xor(h, j, 64);
-            const uint32_t oi = __shfl_xor(id, j, 64);
+    UNR for (int lk = 1; lk <= 6; lk++) {
+        const int k = 1 << lk;
+        if (k > P) break;
+        UNR for (int lj = lk - 1; lj >= 0; lj--) {
+            const int j = 1 << lj;
+            const uint64_t oh = xor_u64(h, j);
+            const uint32_t oi = xor_u32(id, j);
             const bool asc = (lane & k) == 0, lower = (lane & j) == 0;
             const bool other_less = key_less(oh, oi, h, id);
             if ((lower == asc) ? other_less : !other_less) { h = oh; id = oi; }
         }
+    }
     SPHASE(9)
     // term values follow their keys
     UNR for (int e = 0; e < NV; e++) if (e < nv) c[e] = __shfl(c[e], (int)id, 64);
-    const uint64_t prev = __shfl_up(h, 1, 64);
+    const uint64_t prev = prev_u64(h);
     const bool head = lane < N && (lane == 0 || h != prev);
     const unsigned long long hm = __ballot(head);
     const unsigned long long above = lane < 63 ? (hm & ~((2ull << lane) - 1)) : 0ull;
     const int next = above ? __builtin_ctzll(above) : N;
     const int size = head ? next - lane : 0;
-    int maxg = size;
-    UNR for (int m = 32; m > 0; m >>= 1) maxg = max(maxg, __shfl_xor(maxg, m, 64));
-    double acc[9];
-    UNR for (int e = 0; e < 9; e++) acc[e] = c[e];
+    const int maxg = wave_max(size);
+    double acc[9], t[9];
+    UNR for (int e = 0; e < 9; e++) { acc[e] = c[e]; t[e] = c[e]; }
     for (int st = 1; st < maxg; st++) {
-        double t[9];
-        UNR for (int e = 0; e < NV; e++) if (e < nv) t[e] = __shfl(c[e], (lane + st) & 63, 64);
+        // t <- value of lane + 1: after st shifts lane q holds the term at q + st
+        UNR for (int e = 0; e < NV; e++) if (e < nv) t[e] = next_f64(t[e]);
         if (head && st < size) UNR for (int e = 0; e < NV; e++) if (e < nv) acc[e] = acc[e] + t[e];
     }
     SPHASE(10)
@@ -699,9 +701,9 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
         ok = oh.cnt == K;
         x.A->bytes += T.in_bytes() + (double)K * (8.0 + 8.0 * n);
     }
-    hoff = __shfl(hoff, 0, 64);
-    coff = __shfl(coff, 0, 64);
-    ok = __shfl(ok, 0, 64);
+    hoff = bcast0(hoff);
+    coff = bcast0(coff);
+    ok = __builtin_amdgcn_readlane(ok, 0);
     if (ok && keep) {
         x.A->h[hoff + pos] = h;
         double* dst = x.A->c + coff + (long)pos * n;
@@ -743,6 +745,8 @@ __device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const 
             } else if (j < 64 * E) {
                 const int m = j / E;
                 UNR for (int r = 0; r < E; r++) {
+                    // ds_bpermute here: with E keys per lane the exchange is throughput-bound and
+                    // the DPP form (two moves + select per dword) measured slower
                     const uint64_t oh = __shfl_xor(h[r], m, 64);
                     const uint32_t oi = __shfl_xor(id[r], m, 64);
                     const int idx = tid * E + r;
@@ -982,9 +986,9 @@ AI void cross_const(Ctx& x, int o, int a, const CrossC& C) {
             ok = oh.cnt == K;
             x.A->bytes += (double)N * 32.0 + (double)K * 32.0;
         }
-        hoff = __shfl(hoff, 0, 64);
-        coff = __shfl(coff, 0, 64);
-        ok = __shfl(ok, 0, 64);
+        hoff = bcast0(hoff);
+        coff = bcast0(coff);
+        ok = __builtin_amdgcn_readlane(ok, 0);
         if (ok && keep) {
             x.A->h[hoff + pos] = S.h[lane];
             double* dst = x.A->c + coff + (long)pos * 3;
