@@ -14,6 +14,7 @@ namespace armour {
 constexpr int NF = 7;          // trajectory parameters / actuated joints (NUM_FACTORS)
 constexpr int MAX_J = 9;       // largest NUM_JOINTS supported
 constexpr int OBS_GEN = 3;     // MAX_OBSTACLE_GENERATOR_NUM
+constexpr int MAX_OBS = 40;    // MAX_OBSTACLE_NUM (KPR/Parameters.h:26)
 constexpr int BUF_GEN = OBS_GEN + 6;
 constexpr int COMB = BUF_GEN * (BUF_GEN - 1) / 2;  // 36 generator pairs
 

@@ -43,6 +43,7 @@ struct WorldState {
 
 struct NlpDev {
     int W, T, NJ, O, m, R, nblk, chunk;
+    int diag;               // diagnostics (ARMOUR_EVAL_SKIP): bit 0 skip slicing, bit 1 skip collision rows
     const RobotParams* rp;
     IpmOpts opt;
     // per-world inputs
@@ -53,8 +54,6 @@ struct NlpDev {
     const double* obs;      // [W][O][12]
     // reach outputs
     ReachOut ro;
-    // hyperplanes [W][T][NJ][O][COMB], structure of arrays
-    double *hA0, *hA1, *hA2, *hd, *hdel;
     // row bounds [W][R]
     double *L, *U;
     // evaluation slots: g [2][W][m], J [2][W][m][NF], f [2][W], grad [2][W][NF]

@@ -1,8 +1,8 @@
 // armour-mi355x — NLP kernels for a batch of W worlds:
-//   hyperplane_kernel   buffered-obstacle hyperplanes (KPR/CollisionChecking.cu:136-228)
 //   bounds_kernel       constraint bounds (KPR/NLPclass.cu:87-165)
 //   eval_kernel         g(x) and its dense Jacobian (KPR/NLPclass.cu:207-396): PZ slicing
-//                       (PZsparse.cu:404-555), collision rows (CollisionChecking.cu:230-299) with a
+//                       (PZsparse.cu:404-555), collision rows (CollisionChecking.cu:230-299) with
+//                       the buffered-obstacle hyperplanes (:136-228) computed in place and a
 //                       wave-wide argmax in the reference's scan order, torque and extremum rows
 //   ipm_*               armour-IPM (oracle/src/ipm.cpp), one row-parallel pass per phase with
 //                       deterministic block partials and one thread per world for the 7x7 algebra
@@ -57,53 +57,85 @@ __device__ inline double row_va(const NlpDev& d, int slot, int w, int r, const d
     return x[r - d.m];
 }
 
-// ------------------------------------------------------------------------------------------
-// hyperplanes: one thread per (world, t, link, obstacle, generator pair)
-__global__ void hyperplane_kernel(NlpDev d) {
-    const long total = (long)d.W * d.T * d.NJ * d.O * COMB;
-    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-        const int p = (int)(idx % COMB);
-        long rest = idx / COMB;
-        const int o = (int)(rest % d.O); rest /= d.O;
-        const int l = (int)(rest % d.NJ); rest /= d.NJ;
-        const int t = (int)(rest % d.T);
-        const int w = (int)(rest / d.T);
-        // pair table (CollisionChecking.cu:26-39): lexicographic pairs of the 9 buffered generators
-        int a = 0, rem = p;
-        while (rem >= BUF_GEN - 1 - a) { rem -= BUF_GEN - 1 - a; a++; }
-        const int b = a + 1 + rem;
-        const double* ob = d.obs + ((long)w * d.O + o) * 12;
-        const double* lg = d.ro.link_gens + (((long)w * d.T + t) * d.NJ + l) * 18;
-        double G[BUF_GEN][3];
+// plane of the generator pair (ga, gb) (the arithmetic of buffered_plane below, pair given)
+__device__ inline __attribute__((always_inline)) void plane_of(const double* ga, const double* gb, const double (*G)[3],
+                                                               const double* oc, double& C0, double& C1, double& C2,
+                                                               double& dd, double& del) {
+    const double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
+    const double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
+    const double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
+    const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
+    C0 = 0; C1 = 0; C2 = 0;
+    if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
+    dd = C0 * oc[0] + C1 * oc[1] + C2 * oc[2];
+    del = 0.0;
 #pragma unroll
-        for (int i = 0; i < OBS_GEN; i++)
+    for (int j = 0; j < BUF_GEN; j++) del += fabs(C0 * G[j][0] + C1 * G[j][1] + C2 * G[j][2]);
+}
+
+// one monomial's contribution to a slice (k = 0) or to its derivative in x_{k-1}: the products
+// of PZsparse.cu:404-435 / 477-516 in factor order, v * 1.0 standing in for a skipped factor
+__device__ inline __attribute__((always_inline)) double sel4(const double* t, int g) {
+    return g == 0 ? t[0] : (g == 1 ? t[1] : (g == 2 ? t[2] : t[3]));
+}
+__device__ inline __attribute__((always_inline)) double slice_term(double co, int h, int k, const double (*pw)[4],
+                                                                   const double (*dpw)[4]) {
+    double v = co;
+    bool zero = false;
 #pragma unroll
-            for (int r = 0; r < 3; r++) G[i][r] = ob[(i + 1) * 3 + r];
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-#pragma unroll
-            for (int r = 0; r < 3; r++) G[OBS_GEN + i][r] = lg[r + 3 * i];
-        double ga[3], gb[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            ga[r] = G[0][r]; gb[r] = G[1][r];
+    for (int j = 0; j < NF; j++) {
+        const int g = (h >> (2 * j)) & 3;
+        if (j == k - 1) {
+            zero = zero || g == 0;
+            v = v * sel4(dpw[j], g);
+        } else {
+            v = v * sel4(pw[j], g);
         }
-        for (int i = 0; i < BUF_GEN; i++)
-            if (i == a) { ga[0] = G[i][0]; ga[1] = G[i][1]; ga[2] = G[i][2]; }
-        for (int i = 0; i < BUF_GEN; i++)
-            if (i == b) { gb[0] = G[i][0]; gb[1] = G[i][1]; gb[2] = G[i][2]; }
-        double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
-        double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
-        double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
-        const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
-        double C0 = 0, C1 = 0, C2 = 0;
-        if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
-        const double dd = C0 * ob[0] + C1 * ob[1] + C2 * ob[2];
-        double del = 0.0;
-#pragma unroll
-        for (int j = 0; j < BUF_GEN; j++) del += fabs(C0 * G[j][0] + C1 * G[j][1] + C2 * G[j][2]);
-        d.hA0[idx] = C0; d.hA1[idx] = C1; d.hA2[idx] = C2; d.hd[idx] = dd; d.hdel[idx] = del;
     }
+    return zero ? 0.0 : v;
+}
+
+// ------------------------------------------------------------------------------------------
+// hyperplane p of the buffered obstacle (CollisionChecking.cu:136-228): the 9 generators are the
+// obstacle's 3 and the link's 6 (3 box generators + 3 diagonal radii, reduce_link_PZ); plane p is
+// the normalised cross product of the pair (a, b) of the lexicographic pair table (:26-39),
+// d = A . c_obs, delta = sum_k |A . g_k|. Evaluated where it is used (eval_kernel): recomputing
+// costs ~70 flops per plane, streaming a stored plane 40 B.
+__device__ inline void buffered_plane(const double* ob, const double* lg, int p, double& C0, double& C1, double& C2,
+                                      double& dd, double& del) {
+    int a = 0, rem = p;
+    while (rem >= BUF_GEN - 1 - a) { rem -= BUF_GEN - 1 - a; a++; }
+    const int b = a + 1 + rem;
+    double G[BUF_GEN][3];
+#pragma unroll
+    for (int i = 0; i < OBS_GEN; i++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) G[i][r] = ob[(i + 1) * 3 + r];
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) G[OBS_GEN + i][r] = lg[r + 3 * i];
+    double ga[3], gb[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        ga[r] = G[0][r]; gb[r] = G[1][r];
+    }
+#pragma unroll
+    for (int i = 0; i < BUF_GEN; i++)
+        if (i == a) { ga[0] = G[i][0]; ga[1] = G[i][1]; ga[2] = G[i][2]; }
+#pragma unroll
+    for (int i = 0; i < BUF_GEN; i++)
+        if (i == b) { gb[0] = G[i][0]; gb[1] = G[i][1]; gb[2] = G[i][2]; }
+    const double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
+    const double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
+    const double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
+    const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
+    C0 = 0; C1 = 0; C2 = 0;
+    if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
+    dd = C0 * ob[0] + C1 * ob[1] + C2 * ob[2];
+    del = 0.0;
+#pragma unroll
+    for (int j = 0; j < BUF_GEN; j++) del += fabs(C0 * G[j][0] + C1 * G[j][1] + C2 * G[j][2]);
 }
 
 // constraint bounds (NLPclass.cu:87-165); rows m..m+NF-1 are the box bounds on x
@@ -183,86 +215,94 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     if (mode == 1 && !(S.status == 0 && S.searching)) return;
     const int slot = mode == 0 ? 0 : 1 - S.cur;
     const RobotParams& rp = *d.rp;
+    const int tid = threadIdx.x;
+    const long jt = (long)w * d.T + t;
+    const int NJ = d.NJ, O = d.O;
+    // everything this (world, t) reads is staged into LDS with coalesced loads first
     __shared__ double x[NF];
     __shared__ double lc[MAX_J][3];
     __shared__ double dlc[MAX_J][NF][3];
-    if (threadIdx.x < NF) x[threadIdx.x] = mode == 1 ? S.xt[threadIdx.x] : S.x[threadIdx.x];
+    __shared__ double lgen[MAX_J][18];
+    __shared__ double obs[MAX_OBS][12];
+    __shared__ uint16_t lh[MAX_J][CAP_LM];
+    __shared__ double lco[MAX_J][CAP_LM][3];
+    __shared__ uint16_t th[NF][CAP_UM];
+    __shared__ double tco[NF][CAP_UM];
+    __shared__ int lcnt[MAX_J], tcnt[NF];
+    if (tid < NF) x[tid] = mode == 1 ? S.xt[tid] : S.x[tid];
+    if (tid < NJ) lcnt[tid] = d.ro.link_cnt[jt * NJ + tid];
+    if (tid >= 32 && tid < 32 + NF) tcnt[tid - 32] = d.ro.tq_cnt[jt * NF + tid - 32];
+    for (int i = tid; i < NJ * 18; i += blockDim.x) lgen[i / 18][i % 18] = d.ro.link_gens[jt * NJ * 18 + i];
+    for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
     __syncthreads();
-    const long jt = (long)w * d.T + t;
-    // link slices: one thread per (link, component)  (PZsparse.cu:404-435, 477-516)
-    const int tid = threadIdx.x;
-    if (tid < d.NJ * 3) {
-        const int l = tid / 3, e = tid % 3;
-        const long base = jt * d.NJ + l;
-        const int cnt = d.ro.link_cnt[base];
-        double c = d.ro.link_center[base * 3 + e];
-        const double r = d.ro.link_rad[base * 3 + e];
-        double gr[NF];
-#pragma unroll
-        for (int k = 0; k < NF; k++) gr[k] = 0.0;
-        for (int q = 0; q < cnt; q++) {
-            const int h = d.ro.link_hash[base * CAP_LM + q];
-            const double co = d.ro.link_coef[(base * CAP_LM + q) * 3 + e];
-            int dg[NF];
-#pragma unroll
-            for (int j = 0; j < NF; j++) dg[j] = (h >> (2 * j)) & 3;
-            double v = co;
-#pragma unroll
-            for (int j = 0; j < NF; j++) if (dg[j]) v = v * ipow(x[j], dg[j]);
-            c = c + v;
-#pragma unroll
-            for (int k = 0; k < NF; k++) {
-                double tk = co;
-#pragma unroll
-                for (int j = 0; j < NF; j++) {
-                    if (j == k) tk = dg[j] == 0 ? 0.0 : tk * ((double)dg[j] * ipow(x[j], dg[j] - 1));
-                    else if (dg[j]) tk = tk * ipow(x[j], dg[j]);
-                }
-                gr[k] = gr[k] + tk;
+    if (!(d.diag & 1)) {
+        for (int i = tid; i < NJ * CAP_LM; i += blockDim.x) {
+            const int l = i / CAP_LM, q = i % CAP_LM;
+            if (q < lcnt[l]) {
+                const long b = (jt * NJ + l) * CAP_LM + q;
+                lh[l][q] = d.ro.link_hash[b];
+                lco[l][q][0] = d.ro.link_coef[b * 3];
+                lco[l][q][1] = d.ro.link_coef[b * 3 + 1];
+                lco[l][q][2] = d.ro.link_coef[b * 3 + 2];
             }
         }
-        const double cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
-        lc[l][e] = cc;
-        d.link_c[base * 3 + e] = cc;
+        for (int i = tid; i < NF * CAP_UM; i += blockDim.x) {
+            const int j = i / CAP_UM, q = i % CAP_UM;
+            if (q < tcnt[j]) {
+                const long b = (jt * NF + j) * CAP_UM + q;
+                th[j][q] = d.ro.tq_hash[b];
+                tco[j][q] = d.ro.tq_coef[b];
+            }
+        }
+    }
+    __syncthreads();
+    // slices (PZsparse.cu:404-435 value, :477-516 gradient): one thread per output — k = 0 the
+    // value, k = 1..7 the derivative in x_{k-1} — summing its terms in monomial order. Powers come
+    // from per-variable tables, selected without branches: pw[j][g] = x_j^g (g = 0: 1, factor
+    // skipped exactly), dpw[j][g] = g x_j^(g-1), the very products ipow forms.
+    double pw[NF][4], dpw[NF][4];
 #pragma unroll
-        for (int k = 0; k < NF; k++) dlc[l][k][e] = gr[k];
-    } else if (tid >= 64 && tid < 64 + NF) {
+    for (int j = 0; j < NF; j++) {
+        const double xj = x[j];
+        pw[j][0] = 1.0; pw[j][1] = xj; pw[j][2] = xj * xj; pw[j][3] = xj * xj * xj;
+        dpw[j][0] = 0.0; dpw[j][1] = 1.0 * 1.0; dpw[j][2] = 2.0 * xj; dpw[j][3] = 3.0 * (xj * xj);
+    }
+    const int nlk = NJ * 3 * 8;
+    for (int u = tid; u < ((d.diag & 1) ? 0 : nlk + NF * 8); u += blockDim.x) {
+      if (u < nlk) {
+        const int l = u / 24, e = (u / 8) % 3, k = u % 8;
+        const long base = jt * NJ + l;
+        double c = k == 0 ? d.ro.link_center[base * 3 + e] : 0.0;
+        const int cnt = lcnt[l];
+        for (int q = 0; q < cnt; q++) {
+            const int h = lh[l][q];
+            c = c + slice_term(lco[l][q][e], h, k, pw, dpw);
+        }
+        if (k == 0) {
+            const double r = d.ro.link_rad[base * 3 + e];
+            const double cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
+            lc[l][e] = cc;
+            d.link_c[base * 3 + e] = cc;
+        } else {
+            dlc[l][k - 1][e] = c;
+        }
+      } else {
         // torque rows (NLPclass.cu:304-309, 376-380)
-        const int j = tid - 64;
+        const int j = (u - nlk) / 8, k = (u - nlk) % 8;
         const long base = jt * NF + j;
-        const int cnt = d.ro.tq_cnt[base];
-        double c = d.ro.tq_center[base];
-        const double r = d.ro.tq_rad[base];
-        double gr[NF];
-#pragma unroll
-        for (int k = 0; k < NF; k++) gr[k] = 0.0;
-        for (int q = 0; q < cnt; q++) {
-            const int h = d.ro.tq_hash[base * CAP_UM + q];
-            const double co = d.ro.tq_coef[base * CAP_UM + q];
-            int dg[NF];
-#pragma unroll
-            for (int jj = 0; jj < NF; jj++) dg[jj] = (h >> (2 * jj)) & 3;
-            double v = co;
-#pragma unroll
-            for (int jj = 0; jj < NF; jj++) if (dg[jj]) v = v * ipow(x[jj], dg[jj]);
-            c = c + v;
-#pragma unroll
-            for (int k = 0; k < NF; k++) {
-                double tk = co;
-#pragma unroll
-                for (int jj = 0; jj < NF; jj++) {
-                    if (jj == k) tk = dg[jj] == 0 ? 0.0 : tk * ((double)dg[jj] * ipow(x[jj], dg[jj] - 1));
-                    else if (dg[jj]) tk = tk * ipow(x[jj], dg[jj]);
-                }
-                gr[k] = gr[k] + tk;
-            }
+        double c = k == 0 ? d.ro.tq_center[base] : 0.0;
+        const int cnt = tcnt[j];
+        for (int q = 0; q < cnt; q++) c = c + slice_term(tco[j][q], th[j][q], k, pw, dpw);
+        const long gi = gidx(d, slot, w, (long)t * NF + j);
+        if (k == 0) {
+            const double r = d.ro.tq_rad[base];
+            d.g[gi] = ((c - r) + (c + r)) * 0.5;
+        } else {
+            d.J[gi * NF + k - 1] = c;
         }
-        const long row = (long)t * NF + j;
-        const long gi = gidx(d, slot, w, row);
-        d.g[gi] = ((c - r) + (c + r)) * 0.5;
-#pragma unroll
-        for (int k = 0; k < NF; k++) d.J[gi * NF + k] = gr[k];
-    } else if (tid == 128 && t == 0) {
+      }
+    }
+    if (tid == blockDim.x - 1 && t == 0) {
         // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267)
         const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
         const double* q0 = d.q0 + w * NF;
@@ -311,43 +351,51 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         }
     }
     __syncthreads();
-    // collision rows: one wavefront per (link, obstacle); lane p evaluates hyperplane p and the
-    // wave takes the first maximum in the reference's scan order (pos_0, neg_0, pos_1, ...)
-    const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    // collision rows (CollisionChecking.cu:230-299): one thread per (link, obstacle) scans the 36
+    // hyperplanes of the buffered obstacle in the reference's order (pos_p before neg_p, strict
+    // >), so the first maximum wins as in the reference's serial loop
     const long nt = (long)NF * d.T;
-    for (int pr = wave; pr < d.NJ * d.O; pr += nw) {
-        const int l = pr / d.O, o = pr % d.O;
-        const long pb = ((jt * d.NJ + l) * d.O + o) * COMB;
+    for (int pr = tid; pr < ((d.diag & 2) ? 0 : NJ * O); pr += blockDim.x) {
+        const int l = pr / O, o = pr % O;
         double best = -100000000.0;
-        int seq = 1 << 30;
-        double A0 = 0, A1 = 0, A2 = 0;
-        if (lane < COMB) {
-            A0 = d.hA0[pb + lane]; A1 = d.hA1[pb + lane]; A2 = d.hA2[pb + lane];
-            const double dd = d.hd[pb + lane], del = d.hdel[pb + lane];
-            const double nrm = sqrt(A0 * A0 + A1 * A1 + A2 * A2);
-            if (nrm > 0) {
-                const double Ac = A0 * lc[l][0] + A1 * lc[l][1] + A2 * lc[l][2];
-                const double pos = Ac - (dd + del);
-                const double neg = -Ac - (-dd + del);
-                if (pos > best) { best = pos; seq = 2 * lane; }
-                if (neg > best) { best = neg; seq = 2 * lane + 1; }
-            }
-        }
+        double B0 = 0, B1 = 0, B2 = 0;
+        bool isneg = false;
+        const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
+        // the 9 buffered generators in registers: obstacle's 3, then the link's 6
+        double G[BUF_GEN][3], oc[3];
 #pragma unroll
-        for (int m = 1; m < 64; m <<= 1) {
-            const double ob = xor_f64(best, m);
-            const int os = xor_i32(seq, m);
-            if (ob > best || (ob == best && os < seq)) { best = ob; seq = os; }
-        }
-        const int id = seq < (1 << 30) ? (seq >> 1) : 0;
-        const bool isneg = seq < (1 << 30) && (seq & 1);
-        const double B0 = __shfl(A0, id, 64), B1 = __shfl(A1, id, 64), B2 = __shfl(A2, id, 64);
-        const long row = nt + ((long)l * d.T + t) * d.O + o;
+        for (int r = 0; r < 3; r++) oc[r] = obs[o][r];
+#pragma unroll
+        for (int i = 0; i < OBS_GEN; i++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[i][r] = obs[o][(i + 1) * 3 + r];
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[OBS_GEN + i][r] = lgen[l][r + 3 * i];
+        // pairs (a, b), a < b, lexicographic = the pair table's order (CollisionChecking.cu:26-39)
+#pragma unroll
+        for (int a = 0; a < BUF_GEN; a++)
+#pragma unroll
+            for (int b = a + 1; b < BUF_GEN; b++) {
+                double A0, A1, A2, dd, del;
+                plane_of(G[a], G[b], G, oc, A0, A1, A2, dd, del);
+                const double nrm = sqrt(A0 * A0 + A1 * A1 + A2 * A2);
+                if (nrm > 0) {
+                    const double Ac = A0 * c0 + A1 * c1 + A2 * c2;
+                    const double pos = Ac - (dd + del);
+                    const double neg = -Ac - (-dd + del);
+                    if (pos > best) { best = pos; B0 = A0; B1 = A1; B2 = A2; isneg = false; }
+                    if (neg > best) { best = neg; B0 = A0; B1 = A1; B2 = A2; isneg = true; }
+                }
+            }
+        const long row = nt + ((long)l * d.T + t) * O + o;
         const long gi = gidx(d, slot, w, row);
-        if (lane == 0) d.g[gi] = -best;
-        if (lane < NF) {
-            const double dot = B0 * dlc[l][lane][0] + B1 * dlc[l][lane][1] + B2 * dlc[l][lane][2];
-            d.J[gi * NF + lane] = isneg ? dot : -dot;
+        d.g[gi] = -best;
+#pragma unroll
+        for (int k = 0; k < NF; k++) {
+            const double dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
+            d.J[gi * NF + k] = isneg ? dot : -dot;
         }
     }
 }

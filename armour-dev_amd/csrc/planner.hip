@@ -3,7 +3,7 @@
 // One planner handle owns a HIP stream and every device buffer for up to max_worlds worlds of
 // T time steps and max_obstacles obstacles, allocated once (the reference allocates per process,
 // KPR/CollisionChecking.cu:17-53). A batch runs entirely on the device:
-//   reach_kernel (JRS + PZ FK/RNEA + torque radius) -> hyperplane_kernel -> bounds_kernel ->
+//   reach_kernel (JRS + PZ FK/RNEA + torque radius) -> bounds_kernel ->
 //   armour-IPM passes (eval_kernel + ipm_rows_* / ipm_world_*) -> feasible_kernel;
 // the host only sequences launches and reads one flag word per line-search round.
 #include <hip/hip_runtime.h>
@@ -87,7 +87,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     if (cfg->robot != 0) return fail(ARMOUR_E_ARG, "unknown robot id");
     if (cfg->num_time_steps <= 0 || (cfg->num_time_steps % 2) != 0)
         return fail(ARMOUR_E_ARG, "num_time_steps must be a positive even number (KPR/Parameters.h:16)");
-    if (cfg->max_obstacles < 0 || cfg->max_worlds <= 0) return fail(ARMOUR_E_ARG, "bad max_obstacles / max_worlds");
+    if (cfg->max_obstacles < 0 || cfg->max_obstacles > MAX_OBS || cfg->max_worlds <= 0)
+        return fail(ARMOUR_E_ARG, "bad max_obstacles (0..40, MAX_OBSTACLE_NUM) / max_worlds");
     if (cfg->device >= 0) HIPCK(hipSetDevice(cfg->device));
     int dev = 0;
     HIPCK(hipGetDevice(&dev));
@@ -161,16 +162,13 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     // NLP
     NlpDev& d = p->d;
     d.rp = p->d_rp;
+    d.diag = std::getenv("ARMOUR_EVAL_SKIP") ? std::atoi(std::getenv("ARMOUR_EVAL_SKIP")) : 0;
     d.T = T;
     d.NJ = NJ;
     d.ro = ro;
     if (cfg->max_iter > 0) d.opt.max_iter = cfg->max_iter;
     const size_t mmax = (size_t)NF * T + (size_t)T * NJ * Om + NF * 4;
     const size_t Rmax = mmax + NF;
-    const size_t planes = (size_t)Wm * T * NJ * Om * COMB;
-    if ((rc = p->alloc(&d.hA0, planes)) || (rc = p->alloc(&d.hA1, planes)) || (rc = p->alloc(&d.hA2, planes)) ||
-        (rc = p->alloc(&d.hd, planes)) || (rc = p->alloc(&d.hdel, planes)))
-        return rc;
     if ((rc = p->alloc(&d.L, Wm * Rmax)) || (rc = p->alloc(&d.U, Wm * Rmax)) || (rc = p->alloc(&d.g, 2 * Wm * mmax)) ||
         (rc = p->alloc(&d.J, 2 * Wm * mmax * NF)) || (rc = p->alloc(&d.f, 2 * (size_t)Wm)) ||
         (rc = p->alloc(&d.grad, 2 * (size_t)Wm * NF)) || (rc = p->alloc(&d.link_c, jobs * NJ * 3)))
@@ -229,7 +227,7 @@ static int upload_worlds(armour_planner* p, int W, const armour_world* worlds) {
     return 0;
 }
 
-// reach set + hyperplanes + bounds for the uploaded batch
+// reach set + bounds for the uploaded batch
 static int run_reach(armour_planner* p) {
     NlpDev& d = p->d;
     ReachArgs ra = p->ra;
@@ -246,12 +244,6 @@ static int run_reach(armour_planner* p) {
     hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, p->stream, p->d_rp, ra, p->ro);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(p->ev[4], p->stream));
-    if (p->O > 0) {
-        const long planes = (long)p->W * p->T * p->NJ * p->O * COMB;
-        const int blocks = (int)((planes + 255) / 256 < 65535 * 4 ? (planes + 255) / 256 : 65535 * 4);
-        hipLaunchKernelGGL(hyperplane_kernel, dim3(blocks), dim3(256), 0, p->stream, d);
-        HIPCK(hipGetLastError());
-    }
     const long rows = (long)p->W * d.R;
     hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, p->stream, d);
     HIPCK(hipGetLastError());
