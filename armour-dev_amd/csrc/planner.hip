@@ -50,6 +50,7 @@ struct armour_planner {
     hipEvent_t ev[6];
     // reach program (ProgramBuilder::ops) on the device
     Op* d_prog = nullptr;
+    int* d_slot_off = nullptr;
     int nops = 0, nslots = 0;
     unsigned long long* d_bytes = nullptr;
     unsigned long long* d_prof = nullptr;  // per-op [cycles, terms] when ARMOUR_PROFILE_OPS is set
@@ -125,11 +126,17 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     {
         ProgramBuilder pb;
         pb.build(p->rp);
-        if (pb.nslots > MAX_SLOTS) return fail(ARMOUR_E_CAPACITY, "reach program needs more handle slots than MAX_SLOTS");
+        int pool = 0;
+        const std::vector<int> off = pb.slot_offsets(&pool);
+        if (pb.nslots > MAX_SLOTS || pool > POOL_DOUBLES)
+            return fail(ARMOUR_E_CAPACITY, "reach program needs more handle slots / payload pool than the kernel has");
         p->nops = (int)pb.ops.size();
         p->nslots = pb.nslots;
-        if ((rc = p->alloc(&p->d_prog, pb.ops.size())) || (rc = p->alloc(&p->d_bytes, 1))) return rc;
+        if ((rc = p->alloc(&p->d_prog, pb.ops.size())) || (rc = p->alloc(&p->d_bytes, 1)) ||
+            (rc = p->alloc(&p->d_slot_off, off.size())))
+            return rc;
         HIPCK(hipMemcpy(p->d_prog, pb.ops.data(), sizeof(Op) * pb.ops.size(), hipMemcpyHostToDevice));
+        HIPCK(hipMemcpy(p->d_slot_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
         if (std::getenv("ARMOUR_PROFILE_OPS")) {
             if ((rc = p->alloc(&p->d_prof, 2 * pb.ops.size() + 16))) return rc;
             HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 16)));
@@ -140,6 +147,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     ReachArgs& ra = p->ra;
     ra.prog = p->d_prog;
     ra.nops = p->nops;
+    ra.slot_off = p->d_slot_off;
+    ra.nslots = p->nslots;
     ra.bytes = p->d_bytes;
     // ARMOUR_PROFILE_OPS=1: per-op cycles/terms; =2: phase totals (each distorts the other)
     const char* pm = std::getenv("ARMOUR_PROFILE_OPS");

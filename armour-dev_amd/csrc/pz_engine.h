@@ -48,7 +48,9 @@ struct Grp {
 
 // PZ handle. Views: comp >= 0 selects one element of the parent's coefficient block (the
 // reference's operator()(r,c), PZsparse.cu:678-697); scaled applies s * c on read (PZ * double,
-// :996-1030).
+// :996-1030). The handle's small dense blocks live in an LDS pool at `off`, sized by the slot's
+// static shape class n = R*C (1, 3 or 9): centre[n], independent parts ind0[n], ind1[n] and
+// sum_k |m_k| elementwise (absum[n]) — see cen() / ind() / abs_().
 struct PZH {
     int R, C;
     int cnt;
@@ -57,9 +59,7 @@ struct PZH {
     int comp;
     int scaled;
     double scale;
-    double center[9];
-    double ind[2][9];
-    double absum[9];  // sum_k |m_k| elementwise, as the handle presents its monomials
+    int off;
 };
 
 struct Arena {
@@ -73,6 +73,7 @@ struct Arena {
 struct Ctx {
     Grp g;
     PZH* H;            // handle table (LDS)
+    double* pool;      // handle payload pool (LDS)
     Arena* A;          // bump arena state (LDS), storage in HBM
     uint64_t* kh;      // ordered keys: hash        (LDS, cap_lds entries)
     uint32_t* ki;      // ordered keys: term index
@@ -118,6 +119,9 @@ AI void matmul(const double* A, int ra, int ca, const double* B, int cb, double*
 }
 
 AI int nel(const PZH& h) { return h.R * h.C; }
+AI double* cen(const Ctx& x, const PZH& h) { return x.pool + h.off; }
+AI double* ind(const Ctx& x, const PZH& h, int v) { return x.pool + h.off + (1 + v) * (h.R * h.C); }
+AI double* abs_(const Ctx& x, const PZH& h) { return x.pool + h.off + 3 * (h.R * h.C); }
 
 // read monomial k of handle h into a 9-block (entries >= nel(h) are zero)
 AI void read_mono(const Ctx& x, const PZH& h, int k, double* out) {
@@ -470,11 +474,11 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
 }
 
 // output header finish (thread 0): pruned amount into both independent parts (PZsparse.cu:347-349)
-AI void finish_t0(PZH& h, const double* red, const double* abs, int n) {
+AI void finish_t0(const Ctx& x, PZH& h, const double* red, const double* abs, int n) {
     if (frob_norm(red, n) != 0)
         UNR for (int v = 0; v < 2; v++)
-            UNR for (int e = 0; e < 9; e++) if (e < n) h.ind[v][e] = h.ind[v][e] + red[e];
-    UNR for (int e = 0; e < 9; e++) h.absum[e] = e < n ? abs[e] : 0.0;
+            UNR for (int e = 0; e < 9; e++) if (e < n) ind(x, h, v)[e] = ind(x, h, v)[e] + red[e];
+    UNR for (int e = 0; e < 9; e++) if (e < n) abs_(x, h)[e] = abs[e];
 }
 
 AI double frob1(double v) { return frob_norm(&v, 1); }
@@ -506,7 +510,7 @@ struct PolBlock {
         }
         return keep;
     }
-    AI void finish(Ctx& x, int o, const double* red) const { finish_t0(x.H[o], red, red + 9, n); }
+    AI void finish(Ctx& x, int o, const double* red) const { finish_t0(x, x.H[o], red, red + 9, n); }
 };
 
 // fused PZ x PZ cross product of two 3x1 PZs a, b (PZsparse.cu:1118-1167 composes it from element
@@ -578,12 +582,12 @@ struct PolCrossPP {
         const int ea[6] = {1, 2, 2, 0, 0, 1}, fb[6] = {2, 1, 0, 2, 1, 0};
         double pc[6], pi[2][6];
         UNR for (int p = 0; p < 6; p++) {
-            const double ace = pick3(A.center, ea[p]), bcf = pick3(B.center, fb[p]);
-            const double r2 = fabs(ace) + pick3(A.absum, ea[p]);
-            const double r3 = fabs(bcf) + pick3(B.absum, fb[p]);
+            const double ace = pick3(cen(x, A), ea[p]), bcf = pick3(cen(x, B), fb[p]);
+            const double r2 = fabs(ace) + pick3(abs_(x, A), ea[p]);
+            const double r3 = fabs(bcf) + pick3(abs_(x, B), fb[p]);
             pc[p] = ace * bcf;
             UNR for (int v = 0; v < 2; v++) {
-                const double ai = pick3(A.ind[v], ea[p]), bi = pick3(B.ind[v], fb[p]);
+                const double ai = pick3(ind(x, A, v), ea[p]), bi = pick3(ind(x, B, v), fb[p]);
                 pi[v][p] = ai * bi + (r2 * bi + ai * r3);
                 if (frob1(red[p]) != 0) pi[v][p] = pi[v][p] + red[p];
             }
@@ -592,14 +596,14 @@ struct PolCrossPP {
         UNR for (int e = 0; e < 3; e++) sred[e] = red[9 + e];
         const bool sadd = frob_norm(sred, 3) != 0;
         UNR for (int e = 0; e < 3; e++) {
-            h.center[e] = pc[2 * e] - pc[2 * e + 1];
+            cen(x, h)[e] = pc[2 * e] - pc[2 * e + 1];
             UNR for (int v = 0; v < 2; v++) {
                 double iv = pi[v][2 * e] + pi[v][2 * e + 1];
                 if (frob1(red[6 + e]) != 0) iv = iv + red[6 + e];
                 if (sadd) iv = iv + sred[e];
-                h.ind[v][e] = iv;
+                ind(x, h, v)[e] = iv;
             }
-            h.absum[e] = red[12 + e];
+            abs_(x, h)[e] = red[12 + e];
         }
     }
 };
@@ -940,19 +944,19 @@ AI bool cross_const_mono(const CrossC& C, const double* m, double thr, double* o
     return true;
 }
 // header: views (t0_view), differences (PZsparse.cu:813-834), stack, each plus its pruned amount
-AI void cross_const_finish(PZH& h, const PZH& A, const CrossC& C, const double* red) {
+AI void cross_const_finish(const Ctx& x, PZH& h, const PZH& A, const CrossC& C, const double* red) {
     double sred[3];
     UNR for (int e = 0; e < 3; e++) sred[e] = red[3 + e];
     const bool sadd = frob_norm(sred, 3) != 0;
     UNR for (int e = 0; e < 3; e++) {
-        h.center[e] = pick3(A.center, C.iA[e]) * C.sA[e] - pick3(A.center, C.iB[e]) * C.sB[e];
+        cen(x, h)[e] = pick3(cen(x, A), C.iA[e]) * C.sA[e] - pick3(cen(x, A), C.iB[e]) * C.sB[e];
         UNR for (int v = 0; v < 2; v++) {
-            double iv = pick3(A.ind[v], C.iA[e]) * fabs(C.sA[e]) + pick3(A.ind[v], C.iB[e]) * fabs(C.sB[e]);
+            double iv = pick3(ind(x, A, v), C.iA[e]) * fabs(C.sA[e]) + pick3(ind(x, A, v), C.iB[e]) * fabs(C.sB[e]);
             if (frob1(red[e]) != 0) iv = iv + red[e];
             if (sadd) iv = iv + sred[e];
-            h.ind[v][e] = iv;
+            ind(x, h, v)[e] = iv;
         }
-        h.absum[e] = red[6 + e];
+        abs_(x, h)[e] = red[6 + e];
     }
 }
 
@@ -995,7 +999,7 @@ AI void cross_const(Ctx& x, int o, int a, const CrossC& C) {
             UNR for (int e = 0; e < 3; e++) dst[e] = out[e];
         }
         UNR for (int e = 0; e < 9; e++) red[e] = wsum(red[e]);
-        if (lane == 0) cross_const_finish(x.H[o], A, C, red);
+        if (lane == 0) cross_const_finish(x, x.H[o], A, C, red);
         return;
     }
 #endif
@@ -1031,13 +1035,17 @@ AI void cross_const(Ctx& x, int o, int a, const CrossC& C) {
         }
     }
     block_sum_mask(x, red, 9, 0x1ff);
-    if (g.tid == 0) cross_const_finish(x.H[o], A, C, red);
+    if (g.tid == 0) cross_const_finish(x, x.H[o], A, C, red);
 }
 
-AI void hdr_init(PZH& h, int R, int C) {
+// header of an empty R x C PZ; the slot's payload class must be R*C (the program builder's shape
+// classes guarantee it). Keeps `off`.
+AI void hdr_init(const Ctx& x, PZH& h, int R, int C) {
     h.R = R; h.C = C; h.cnt = 0; h.stride = R * C; h.hoff = 0; h.coff = 0;
     h.comp = -1; h.scaled = 0; h.scale = 1.0;
-    UNR for (int e = 0; e < 9; e++) { h.center[e] = 0.0; h.ind[0][e] = 0.0; h.ind[1][e] = 0.0; h.absum[e] = 0.0; }
+    double* p = cen(x, h);
+    const int n = R * C;
+    UNR for (int e = 0; e < 36; e++) if (e < 4 * n) p[e] = 0.0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1059,13 +1067,13 @@ AI void header_add(Ctx& x, int o, int a, int b, int sign) {
     const PZH& A = x.H[a];
     const PZH& B = x.H[b];
     PZH& h = x.H[o];
-    hdr_init(h, A.R, A.C);
+    hdr_init(x, h, A.R, A.C);
     const int n = nel(A);
     UNR for (int e = 0; e < 9; e++) {
         if (e < n) {
-            h.center[e] = sign > 0 ? A.center[e] + B.center[e] : A.center[e] - B.center[e];
-            h.ind[0][e] = A.ind[0][e] + B.ind[0][e];
-            h.ind[1][e] = A.ind[1][e] + B.ind[1][e];
+            cen(x, h)[e] = sign > 0 ? cen(x, A)[e] + cen(x, B)[e] : cen(x, A)[e] - cen(x, B)[e];
+            ind(x, h, 0)[e] = ind(x, A, 0)[e] + ind(x, B, 0)[e];
+            ind(x, h, 1)[e] = ind(x, A, 1)[e] + ind(x, B, 1)[e];
         }
     }
 }
@@ -1077,7 +1085,7 @@ AI void terms_mul(const Ctx& x, int a, int b, Terms& T) {
     T.kind = 0; T.ns = 2;
     T.places = 0; T.negs = 0;
     T.S[0] = src_of(x, A); T.S[1] = src_of(x, B);
-    T.Ac = A.center; T.Bc = B.center;
+    T.Ac = cen(x, A); T.Bc = cen(x, B);
     T.AR = A.R; T.AC = A.C; T.BC = B.C;
     const bool as = A.R == 1 && A.C == 1, bs = B.R == 1 && B.C == 1;
     T.nout = as ? nel(B) : (bs ? nel(A) : A.R * B.C);
@@ -1089,20 +1097,20 @@ AI void header_mul(Ctx& x, int o, int a, int b, const Terms& T) {
     const PZH& B = x.H[b];
     const bool as = A.R == 1 && A.C == 1, bs = B.R == 1 && B.C == 1;
     PZH& h = x.H[o];
-    hdr_init(h, as ? B.R : A.R, as ? B.C : (bs ? A.C : B.C));
+    hdr_init(x, h, as ? B.R : A.R, as ? B.C : (bs ? A.C : B.C));
     const int na = nel(A), nb = nel(B), nr = nel(h);
-    double cen[9], ac[9], bc[9], r2[9], r3[9];
+    double cv[9], ac[9], bc[9], r2[9], r3[9];
     UNR for (int e = 0; e < 9; e++) {
-        ac[e] = A.center[e];
-        bc[e] = B.center[e];
-        r2[e] = e < na ? fabs(A.center[e]) + A.absum[e] : 0.0;
-        r3[e] = e < nb ? fabs(B.center[e]) + B.absum[e] : 0.0;
+        ac[e] = cen(x, A)[e];
+        bc[e] = cen(x, B)[e];
+        r2[e] = e < na ? fabs(cen(x, A)[e]) + abs_(x, A)[e] : 0.0;
+        r3[e] = e < nb ? fabs(cen(x, B)[e]) + abs_(x, B)[e] : 0.0;
     }
-    T.prod(ac, bc, cen);
-    UNR for (int e = 0; e < 9; e++) if (e < nr) h.center[e] = cen[e];
+    T.prod(ac, bc, cv);
+    UNR for (int e = 0; e < 9; e++) if (e < nr) cen(x, h)[e] = cv[e];
     UNR for (int v = 0; v < 2; v++) {
         double ai[9], bi[9], t2[9], t3[9], ii[9];
-        UNR for (int e = 0; e < 9; e++) { ai[e] = A.ind[v][e]; bi[e] = B.ind[v][e]; }
+        UNR for (int e = 0; e < 9; e++) { ai[e] = ind(x, A, v)[e]; bi[e] = ind(x, B, v)[e]; }
         if (as) {
             UNR for (int e = 0; e < 9; e++) { t2[e] = r2[0] * bi[e]; t3[e] = ai[0] * r3[e]; ii[e] = ai[0] * bi[e]; }
         } else if (bs) {
@@ -1112,7 +1120,7 @@ AI void header_mul(Ctx& x, int o, int a, int b, const Terms& T) {
             matmul(ai, A.R, A.C, r3, B.C, t3);
             matmul(ai, A.R, A.C, bi, B.C, ii);
         }
-        UNR for (int e = 0; e < 9; e++) if (e < nr) h.ind[v][e] = ii[e] + (t2[e] + t3[e]);
+        UNR for (int e = 0; e < 9; e++) if (e < nr) ind(x, h, v)[e] = ii[e] + (t2[e] + t3[e]);
     }
     if (as && !bs && B.R != 1 && A.cnt > 0 && B.cnt > 0) *x.err |= ERR_HANDLES;  // Eigen assert in the reference
     if (!as && !bs && !(A.R == 3 && A.C == 3 && B.R == 3)) *x.err |= ERR_HANDLES;  // block shape outside matmul()
@@ -1126,7 +1134,7 @@ AI void terms_cross_pp(const Ctx& x, int a, int b, Terms& T) {
     T.kind = 0; T.ns = 2;
     T.places = 0; T.negs = 0;
     T.S[0] = src_of(x, A); T.S[1] = src_of(x, B);
-    T.Ac = A.center; T.Bc = B.center;
+    T.Ac = cen(x, A); T.Bc = cen(x, B);
     T.AR = 3; T.AC = 1; T.BC = 1;
     T.nout = 3;
 }
@@ -1144,10 +1152,10 @@ AI void header_stack3(Ctx& x, int o, int a0, int a1, int a2) {
     const PZH& S1 = x.H[a1];
     const PZH& S2 = x.H[a2];
     PZH& h = x.H[o];
-    hdr_init(h, 3, 1);
-    h.center[0] = S0.center[0]; h.ind[0][0] = S0.ind[0][0]; h.ind[1][0] = S0.ind[1][0];
-    h.center[1] = S1.center[0]; h.ind[0][1] = S1.ind[0][0]; h.ind[1][1] = S1.ind[1][0];
-    h.center[2] = S2.center[0]; h.ind[0][2] = S2.ind[0][0]; h.ind[1][2] = S2.ind[1][0];
+    hdr_init(x, h, 3, 1);
+    cen(x, h)[0] = cen(x, S0)[0]; ind(x, h, 0)[0] = ind(x, S0, 0)[0]; ind(x, h, 1)[0] = ind(x, S0, 1)[0];
+    cen(x, h)[1] = cen(x, S1)[0]; ind(x, h, 0)[1] = ind(x, S1, 0)[0]; ind(x, h, 1)[1] = ind(x, S1, 1)[0];
+    cen(x, h)[2] = cen(x, S2)[0]; ind(x, h, 0)[2] = ind(x, S2, 0)[0]; ind(x, h, 1)[2] = ind(x, S2, 1)[0];
 }
 
 // self(e) += a (1x1)  (PZsparse.cu:1068-1085)
@@ -1163,12 +1171,14 @@ AI void header_add_one_dim(Ctx& x, int o, int self, int a, int e) {
     const PZH& A = x.H[self];
     const PZH& B = x.H[a];
     PZH& h = x.H[o];
-    hdr_init(h, A.R, A.C);
+    hdr_init(x, h, A.R, A.C);
+    const int n = nel(A);
     UNR for (int q = 0; q < 9; q++) {
+        if (q >= n) break;
         const bool at = q == e;
-        h.center[q] = at ? A.center[q] + B.center[0] : A.center[q];
-        h.ind[0][q] = at ? A.ind[0][q] + B.ind[0][0] : A.ind[0][q];
-        h.ind[1][q] = at ? A.ind[1][q] + B.ind[1][0] : A.ind[1][q];
+        cen(x, h)[q] = at ? cen(x, A)[q] + cen(x, B)[0] : cen(x, A)[q];
+        ind(x, h, 0)[q] = at ? ind(x, A, 0)[q] + ind(x, B, 0)[0] : ind(x, A, 0)[q];
+        ind(x, h, 1)[q] = at ? ind(x, A, 1)[q] + ind(x, B, 1)[0] : ind(x, A, 1)[q];
     }
 }
 

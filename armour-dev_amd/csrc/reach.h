@@ -227,12 +227,12 @@ T0FN void t0_make_raw(Ctx& x, int o, int R, int C, const double* center, int nc,
         i = j;
     }
     PZH& h = x.H[o];
-    hdr_init(h, R, C);
-    for (int e = 0; e < n; e++) h.center[e] = center[e];
+    hdr_init(x, h, R, C);
+    for (int e = 0; e < n; e++) cen(x, h)[e] = center[e];
     if (frob_norm(red, n) != 0)
-        for (int e = 0; e < n; e++) { h.ind[0][e] += red[e]; h.ind[1][e] += red[e]; }
+        for (int e = 0; e < n; e++) { ind(x, h, 0)[e] += red[e]; ind(x, h, 1)[e] += red[e]; }
     for (int k = 0; k < K; k++)
-        for (int e = 0; e < n; e++) h.absum[e] += fabs(keep_c[k][e]);
+        for (int e = 0; e < n; e++) abs_(x, h)[e] += fabs(keep_c[k][e]);
     arena_alloc_t0(x, h, K, n);
     if (h.cnt == K)
         for (int k = 0; k < K; k++) {
@@ -245,11 +245,11 @@ T0FN void t0_make_raw(Ctx& x, int o, int R, int C, const double* center, int nc,
 // the uncertainty enters only the interval part (ind[1]) of the fused nominal/interval pair
 T0FN void t0_const(Ctx& x, int o, int R, int C, const double* center, double unc_int) {
     PZH& h = x.H[o];
-    hdr_init(h, R, C);
+    hdr_init(x, h, R, C);
     const int n = R * C;
     for (int e = 0; e < n; e++) {
-        h.center[e] = center[e];
-        h.ind[1][e] = unc_int * fabs(center[e]);
+        cen(x, h)[e] = center[e];
+        ind(x, h, 1)[e] = unc_int * fabs(center[e]);
     }
 }
 
@@ -266,13 +266,11 @@ T0FN void t0_view(Ctx& x, int o, int a, int e, int scaled, double s) {
     h.scaled = scaled;
     h.scale = scaled ? s : 1.0;
     if (P.comp >= 0 || P.scaled) *x.err |= ERR_HANDLES;  // views of views never occur in this program
-    for (int q = 0; q < 9; q++) {
+    for (int q = 0; q < n; q++) {
         const int src = e >= 0 ? e : q;
-        double c = 0.0, i0 = 0.0, i1 = 0.0;
-        if (q < n) { c = P.center[src]; i0 = P.ind[0][src]; i1 = P.ind[1][src]; }
-        double ab = q < n ? P.absum[src] : 0.0;
+        double c = cen(x, P)[src], i0 = ind(x, P, 0)[src], i1 = ind(x, P, 1)[src], ab = abs_(x, P)[src];
         if (scaled) { c = c * s; i0 = i0 * fabs(s); i1 = i1 * fabs(s); ab = ab * fabs(s); }
-        h.center[q] = c; h.ind[0][q] = i0; h.ind[1][q] = i1; h.absum[q] = ab;
+        cen(x, h)[q] = c; ind(x, h, 0)[q] = i0; ind(x, h, 1)[q] = i1; abs_(x, h)[q] = ab;
     }
 }
 
@@ -281,13 +279,13 @@ T0FN void t0_view(Ctx& x, int o, int a, int e, int scaled, double s) {
 T0FN void t0_transpose(Ctx& x, int o, int a) {
     const PZH& A = x.H[a];
     PZH& h = x.H[o];
-    hdr_init(h, A.C, A.R);
+    hdr_init(x, h, A.C, A.R);
     for (int i = 0; i < A.R; i++)
         for (int j = 0; j < A.C; j++) {
-            h.center[j + i * A.C] = A.center[i + j * A.R];
-            h.ind[0][j + i * A.C] = A.ind[0][i + j * A.R];
-            h.ind[1][j + i * A.C] = A.ind[1][i + j * A.R];
-            h.absum[j + i * A.C] = A.absum[i + j * A.R];
+            cen(x, h)[j + i * A.C] = cen(x, A)[i + j * A.R];
+            ind(x, h, 0)[j + i * A.C] = ind(x, A, 0)[i + j * A.R];
+            ind(x, h, 1)[j + i * A.C] = ind(x, A, 1)[i + j * A.R];
+            abs_(x, h)[j + i * A.C] = abs_(x, A)[i + j * A.R];
         }
     const int n = nel(A);
     arena_alloc_t0(x, h, A.cnt, n);
@@ -355,7 +353,7 @@ T0FN void t0_emit_link(Ctx& x, const ReachOut& out, long j, int a, int l) {
     double gl[18];
     for (int e = 0; e < 18; e++) gl[e] = 0.0;
     int jg = 0, kk = 0;
-    double ind[3] = {h.ind[0][0], h.ind[0][1], h.ind[0][2]};
+    double rad[3] = {ind(x, h, 0)[0], ind(x, h, 0)[1], ind(x, h, 0)[2]};
     for (int k = 0; k < h.cnt; k++) {
         const uint64_t hh = x.A->h[h.hoff + k];
         const double* c = x.A->c + h.coff + (long)k * 3;
@@ -372,15 +370,15 @@ T0FN void t0_emit_link(Ctx& x, const ReachOut& out, long j, int a, int l) {
             else *x.err |= ERR_LINKGEN;
             jg++;
         } else {
-            for (int e = 0; e < 3; e++) ind[e] += fabs(c[e]);
+            for (int e = 0; e < 3; e++) rad[e] += fabs(c[e]);
         }
     }
-    gl[0 + 3 * 3] = ind[0];
-    gl[1 + 3 * 4] = ind[1];
-    gl[2 + 3 * 5] = ind[2];
+    gl[0 + 3 * 3] = rad[0];
+    gl[1 + 3 * 4] = rad[1];
+    gl[2 + 3 * 5] = rad[2];
     for (int e = 0; e < 18; e++) gens[e] = gl[e];
     out.link_cnt[base] = kk < CAP_LM ? kk : CAP_LM;
-    for (int e = 0; e < 3; e++) { out.link_center[base * 3 + e] = h.center[e]; out.link_rad[base * 3 + e] = ind[e]; }
+    for (int e = 0; e < 3; e++) { out.link_center[base * 3 + e] = cen(x, h)[e]; out.link_rad[base * 3 + e] = rad[e]; }
 }
 
 T0FN void t0_emit_torque(Ctx& x, const ReachOut& out, long j, int a, int i, double* rdist, double* ured) {
@@ -388,9 +386,9 @@ T0FN void t0_emit_torque(Ctx& x, const ReachOut& out, long j, int a, int i, doub
     const long base = j * NF + i;
     // disturbance u_int - u_nom: centres and monomials cancel exactly, the independent parts add
     // (armour_main.cu:135-137, PZsparse.cu:813-834)
-    rdist[i] = h.ind[1][0] + h.ind[0][0];
+    rdist[i] = ind(x, h, 1)[0] + ind(x, h, 0)[0];
     // reduce (PZsparse.cu:352-368)
-    double ind = h.ind[0][0];
+    double rad = ind(x, h, 0)[0];
     int kk = 0;
     for (int k = 0; k < h.cnt; k++) {
         const uint64_t hh = x.A->h[h.hoff + k];
@@ -405,13 +403,13 @@ T0FN void t0_emit_torque(Ctx& x, const ReachOut& out, long j, int a, int i, doub
             }
             kk++;
         } else {
-            ind += fabs(c);
+            rad += fabs(c);
         }
     }
     out.tq_cnt[base] = kk < CAP_UM ? kk : CAP_UM;
-    out.tq_center[base] = h.center[0];
-    out.tq_rad[base] = ind;
-    ured[i] = ind;
+    out.tq_center[base] = cen(x, h)[0];
+    out.tq_rad[base] = rad;
+    ured[i] = rad;
 }
 
 // torque radius (armour_main.cu:173-211)
@@ -501,8 +499,8 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                 break;
             case OP_ZERO:
                 if (tid == 0) {
-                    hdr_init(x.H[op.o], op.b, op.c);
-                    if (op.i) x.H[op.o].center[2] = rp.gravity;
+                    hdr_init(x, x.H[op.o], op.b, op.c);
+                    if (op.i) cen(x, x.H[op.o])[2] = rp.gravity;
                 }
                 break;
             case OP_VIEW: if (tid == 0) t0_view(x, op.o, op.a, op.i, op.b, op.s); break;
@@ -513,7 +511,7 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
             case OP_CROSS_C: {
                 const double* v = op.b == VEC_TRANS ? &rp.trans[3 * op.c] : &rp.com[3 * op.c];
                 const CrossC C = cross_const_table(op.i, v);
-                if (tid == 0) hdr_init(x.H[op.o], 3, 1);
+                if (tid == 0) hdr_init(x, x.H[op.o], 3, 1);
                 cross_const(x, op.o, op.a, C);
                 break;
             }
@@ -523,11 +521,11 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                 const int N = op_terms(x, op);
                 PolCrossPP pol;
                 pol.thr = x.thr;
-                pol.ac = x.H[op.a].center;
-                pol.bc = x.H[op.b].center;
+                pol.ac = cen(x, x.H[op.a]);
+                pol.bc = cen(x, x.H[op.b]);
                 pol.a = op.a;
                 pol.b = op.b;
-                if (tid == 0) hdr_init(x.H[op.o], 3, 1);
+                if (tid == 0) hdr_init(x, x.H[op.o], 3, 1);
 #if defined(__HIP_DEVICE_COMPILE__)
                 if (N <= 64 && !(x.mode & 1)) {
                     if (tid < 64) simplify_small(x, op.o, Tm, pol, N);
@@ -576,8 +574,8 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
             if (tid == 0) {
                 const PZH& h = x.H[op.o];
                 double* d = dump + (long)pc * DUMP_W;
-                d[0] = h.cnt; d[1] = h.R * h.C; d[2] = h.center[0]; d[3] = h.center[1]; d[4] = h.center[2];
-                d[5] = h.ind[0][0]; d[6] = h.ind[1][0]; d[7] = h.absum[0];
+                d[0] = h.cnt; d[1] = h.R * h.C; d[2] = cen(x, h)[0]; d[3] = cen(x, h)[1]; d[4] = cen(x, h)[2];
+                d[5] = ind(x, h, 0)[0]; d[6] = ind(x, h, 1)[0]; d[7] = abs_(x, h)[0];
             }
             x.g.sync();
         }
@@ -598,14 +596,42 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 // ---- host: program builder --------------------------------------------------------------------
 struct ProgramBuilder {
     std::vector<Op> ops;
-    std::vector<int> free_slots;
+    // handle slots, SSA style: every op writes a fresh (or freed) slot, so no op's output aliases
+    // an operand. Each slot has a fixed payload class n = R*C (1, 3 or 9), so the LDS payload pool
+    // holds 4n doubles per slot instead of the 3x3 worst case.
+    std::vector<int> cls;
+    std::vector<int> free_by[10];
     int nslots = 0;
 
-    int alloc() {
-        if (!free_slots.empty()) { const int s = free_slots.back(); free_slots.pop_back(); return s; }
+    int alloc(int n) {
+        if (!free_by[n].empty()) { const int s = free_by[n].back(); free_by[n].pop_back(); return s; }
+        cls.push_back(n);
         return nslots++;
     }
-    void rel(int s) { free_slots.push_back(s); }
+    void rel(int s) { free_by[cls[s]].push_back(s); }
+    // payload offsets (doubles) of every slot in the pool, and the pool size
+    std::vector<int> slot_offsets(int* total) const {
+        std::vector<int> off(nslots);
+        int acc = 0;
+        for (int k = 0; k < nslots; k++) { off[k] = acc; acc += 4 * cls[k]; }
+        *total = acc;
+        return off;
+    }
+    int out_class(int code, int a, int b, int c, int i) const {
+        switch (code) {
+            case OP_MUL: {
+                const int ca = cls[a], cb = cls[b];
+                return ca == 1 ? cb : (cb == 1 ? ca : (cb == 9 ? 9 : 3));
+            }
+            case OP_ADD: case OP_ADD1D: case OP_TRANSPOSE: return cls[a];
+            case OP_VIEW: return i >= 0 ? 1 : cls[a];
+            case OP_CONST: return (a == CONST_RPY || a == CONST_INERTIA) ? 9 : (a == CONST_TRANS ? 3 : 1);
+            case OP_ZERO: return b * c;
+            case OP_MAKE1D: return 1;
+            case OP_MAKEROT: return 9;
+            default: return 3;  // MAKEBOX, STACK3, CROSS_C, CROSS_PP
+        }
+    }
     void rel(std::initializer_list<int> l) { for (int s : l) rel(s); }
     void emit(int code, int o = -1, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
         Op op;
@@ -613,7 +639,7 @@ struct ProgramBuilder {
         ops.push_back(op);
     }
     int out(int code, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
-        const int o = alloc();
+        const int o = alloc(out_class(code, a, b, c, i));
         emit(code, o, a, b, c, i, s);
         return o;
     }

@@ -10,6 +10,7 @@ namespace armour {
 constexpr int REACH_THREADS = 256;
 constexpr int KEY_CAP_LDS = 2048;
 constexpr int STAGE_DOUBLES = 2560;
+constexpr int POOL_DOUBLES = 1536;   // handle payloads (ProgramBuilder::slot_offsets)
 
 struct ReachArgs {
     int W, T;
@@ -18,6 +19,8 @@ struct ReachArgs {
     const double* qdd0;
     const Op* prog;      // reach program (device copy of ProgramBuilder::ops)
     int nops;
+    const int* slot_off; // payload offset of every handle slot in the LDS pool
+    int nslots;
     uint64_t* arena_h;   // [grid][arena_cap]
     double* arena_c;     // [grid][arena_cap * 3]
     long arena_cap;
@@ -34,6 +37,7 @@ struct ReachArgs {
 
 __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
     __shared__ PZH H[MAX_SLOTS];
+    __shared__ double pool[POOL_DOUBLES + 9];  // + 9: header reads of a full 3x3 past a small slot
     __shared__ uint64_t kh[KEY_CAP_LDS];
     __shared__ uint32_t ki[KEY_CAP_LDS];
     __shared__ int kp[KEY_CAP_LDS];
@@ -51,7 +55,9 @@ __global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotPara
     Ctx x;
     x.g = Grp{(int)threadIdx.x, (int)blockDim.x};
     x.H = H;
+    x.pool = pool;
     x.A = &arena;
+    for (int k = threadIdx.x; k < a.nslots; k += blockDim.x) H[k].off = a.slot_off[k];
     x.kh = kh; x.ki = ki; x.kp = kp; x.cap_lds = KEY_CAP_LDS;
     x.gkh = a.gkh + (long)blockIdx.x * a.gcap;
     x.gki = a.gki + (long)blockIdx.x * a.gcap;

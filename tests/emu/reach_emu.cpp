@@ -31,6 +31,10 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     std::vector<uint64_t> ah(cap);
     std::vector<double> ac(cap * 3);
     std::vector<PZH> H(pb.nslots);
+    int pool_n = 0;
+    const std::vector<int> off = pb.slot_offsets(&pool_n);
+    std::vector<double> pool(pool_n + 9);
+    for (int k = 0; k < pb.nslots; k++) H[k].off = off[k];
     const int kcap = 1 << 16;
     std::vector<uint64_t> kh(kcap);
     std::vector<uint32_t> ki(kcap);
@@ -42,6 +46,7 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     Ctx x;
     x.g = Grp{0, 1};
     x.H = H.data();
+    x.pool = pool.data();
     x.A = &A;
     x.kh = kh.data(); x.ki = ki.data(); x.kp = kp.data(); x.cap_lds = kcap;
     x.gkh = kh.data(); x.gki = ki.data(); x.gkp = kp.data(); x.cap_glb = kcap;
@@ -70,4 +75,20 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     if (nops) *nops = (int)pb.ops.size();
     if (nslots) *nslots = pb.nslots;
     return err;
+}
+
+// the op program (code, o, a, b, c, i) of the fused (or composed) build, for analysis tools
+extern "C" int emu_program(int unfused, int* out, int cap) {
+    static RobotParams rp;
+    kinova_gen3(rp);
+    ProgramBuilder pb;
+    pb.fused = !unfused;
+    pb.build(rp);
+    const int n = (int)pb.ops.size();
+    for (int k = 0; k < n && k < cap; k++) {
+        const Op& op = pb.ops[k];
+        out[6 * k] = op.code; out[6 * k + 1] = op.o; out[6 * k + 2] = op.a;
+        out[6 * k + 3] = op.b; out[6 * k + 4] = op.c; out[6 * k + 5] = op.i;
+    }
+    return n;
 }
