@@ -142,8 +142,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
             HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 16)));
         }
     }
-    // reach workspace: two resident workgroups per CU, each with a private arena
-    p->reach_grid = 2 * p->ncu;
+    // reach workspace: four resident workgroups per CU, each with a private arena
+    p->reach_grid = 4 * p->ncu;
     ReachArgs& ra = p->ra;
     ra.prog = p->d_prog;
     ra.nops = p->nops;

@@ -721,8 +721,10 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
 }
 
 // ---- register bitonic: 256 x E keys, E per thread (element index tid * E + r) -----------------
+// xh/xi: exchange buffers for the cross-wave stages (>= P entries), oh/oi: the ordered output
 template <int E>
-__device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const Terms& T, int N) {
+__device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const Terms& T, int N, uint64_t* xh, uint32_t* xi,
+                                                                  uint64_t* oh, uint32_t* oi) {
     const int tid = x.g.tid;
     uint64_t h[E];
     uint32_t id[E];
@@ -759,22 +761,22 @@ __device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const 
                     if ((lower == asc) ? other_less : !other_less) { h[r] = oh; id[r] = oi; }
                 }
             } else {
-                UNR for (int r = 0; r < E; r++) { x.kh[tid * E + r] = h[r]; x.ki[tid * E + r] = id[r]; }
+                UNR for (int r = 0; r < E; r++) { xh[tid * E + r] = h[r]; xi[tid * E + r] = id[r]; }
                 x.g.sync();
                 UNR for (int r = 0; r < E; r++) {
                     const int idx = tid * E + r;
-                    const uint64_t oh = x.kh[idx ^ j];
-                    const uint32_t oi = x.ki[idx ^ j];
+                    const uint64_t ph = xh[idx ^ j];
+                    const uint32_t pi = xi[idx ^ j];
                     const bool asc = (idx & k) == 0, lower = (idx & j) == 0;
-                    const bool other_less = key_less(oh, oi, h[r], id[r]);
-                    if ((lower == asc) ? other_less : !other_less) { h[r] = oh; id[r] = oi; }
+                    const bool other_less = key_less(ph, pi, h[r], id[r]);
+                    if ((lower == asc) ? other_less : !other_less) { h[r] = ph; id[r] = pi; }
                 }
                 x.g.sync();
             }
         }
     UNR for (int r = 0; r < E; r++) {
         const int idx = tid * E + r;
-        if (idx < N) { x.kh[idx] = h[r]; x.ki[idx] = id[r]; }
+        if (idx < N) { oh[idx] = h[r]; oi[idx] = id[r]; }
     }
 }
 #endif
@@ -826,12 +828,17 @@ AI void simplify_big(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
         }
     }
 #if defined(__HIP_DEVICE_COMPILE__)
-    else if (in_lds) {
-        const int E = N <= 256 ? 1 : N <= 512 ? 2 : N <= 1024 ? 4 : 8;
-        if (E == 1) reg_bitonic<1>(x, T, N);
-        else if (E == 2) reg_bitonic<2>(x, T, N);
-        else if (E == 4) reg_bitonic<4>(x, T, N);
-        else reg_bitonic<8>(x, T, N);
+    else if (N <= 16 * g.n) {
+        // register bitonic over g.n * E keys; keys and exchanges in LDS up to its capacity, the
+        // rare larger operator exchanges and lands in the global buffers
+        const int E = N <= g.n ? 1 : N <= 2 * g.n ? 2 : N <= 4 * g.n ? 4 : N <= 8 * g.n ? 8 : 16;
+        uint64_t* xh = E * g.n <= x.cap_lds ? x.kh : x.gkh;
+        uint32_t* xi = E * g.n <= x.cap_lds ? x.ki : x.gki;
+        if (E == 1) reg_bitonic<1>(x, T, N, xh, xi, kh, ki);
+        else if (E == 2) reg_bitonic<2>(x, T, N, xh, xi, kh, ki);
+        else if (E == 4) reg_bitonic<4>(x, T, N, xh, xi, kh, ki);
+        else if (E == 8) reg_bitonic<8>(x, T, N, xh, xi, kh, ki);
+        else reg_bitonic<16>(x, T, N, xh, xi, kh, ki);
     }
 #endif
     else {

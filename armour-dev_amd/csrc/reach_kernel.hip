@@ -1,16 +1,17 @@
-// armour-mi355x — reach-set kernel: one 256-thread workgroup per (world, time interval) job.
+// armour-mi355x — reach-set kernel: one 128-thread workgroup per (world, time interval) job.
 // Persistent grid: each workgroup walks jobs job = blockIdx.x + k * gridDim.x, interprets the
 // reach program (reach.h) for each, and owns a private HBM arena (monomial storage) plus a global
-// fallback sort buffer for products larger than the LDS key buffer. LDS (~78 KB) holds the PZ
-// handle table, the (hash, index) keys and the operand staging buffer, so two workgroups fit per CU.
+// fallback sort buffer for products larger than the LDS key buffer. LDS (< 40 KB) holds the PZ
+// handle table and payload pool, the (hash, index) keys and the operand staging buffer, so four
+// workgroups (eight waves) fit per CU — the VGPR budget of two waves per SIMD.
 #include "reach.h"
 
 namespace armour {
 
-constexpr int REACH_THREADS = 256;
-constexpr int KEY_CAP_LDS = 2048;
-constexpr int STAGE_DOUBLES = 2560;
-constexpr int POOL_DOUBLES = 1536;   // handle payloads (ProgramBuilder::slot_offsets)
+constexpr int REACH_THREADS = 128;   // two waves per job, four jobs resident per CU
+constexpr int KEY_CAP_LDS = 1024;
+constexpr int STAGE_DOUBLES = 1280;
+constexpr int POOL_DOUBLES = 1024;   // handle payloads (ProgramBuilder::slot_offsets)
 
 struct ReachArgs {
     int W, T;
@@ -35,7 +36,8 @@ struct ReachArgs {
     double* dump;               // optional op-by-op state of job 0 (null: off)
 };
 
-__global__ __launch_bounds__(REACH_THREADS, 2) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
+// 2 waves per SIMD: 256 registers per lane (VGPR + AGPR), four 2-wave workgroups per CU
+__global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREADS), amdgpu_waves_per_eu(2, 2))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
     __shared__ PZH H[MAX_SLOTS];
     __shared__ double pool[POOL_DOUBLES + 9];  // + 9: header reads of a full 3x3 past a small slot
     __shared__ uint64_t kh[KEY_CAP_LDS];
