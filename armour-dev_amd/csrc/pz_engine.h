@@ -490,27 +490,30 @@ AI double pick3(const double* m, int i) { return i == 0 ? m[0] : (i == 1 ? m[1] 
 // keep / prune; NR reduction slots (a bit mask says which are live); finish() completes the
 // output header from the reduced slots (thread 0).
 
-// plain simplify (PZsparse.cu:284-350): group sum of coefficient blocks, prune by Frobenius norm
+// plain simplify (PZsparse.cu:284-350): group sum of coefficient blocks, prune by Frobenius norm.
+// Instantiated per output class NN (1x1, 3x1, 3x3) so the frequent small blocks carry no 9-element
+// arrays: the register budget of the common paths stays clear of the 3x3 one.
+template <int NN>
 struct PolBlock {
-    static constexpr int NV = 9;
-    static constexpr int NR = 18;   // [0, 9): pruned |sum|, [9, 18): kept |sum| (absum)
-    int n;
+    static constexpr int NV = NN;
+    static constexpr int NO = NN;
+    static constexpr int NR = 2 * NN;   // [0, NN): pruned |sum|, [NN, 2NN): kept |sum| (absum)
     double thr;
-    AI int nv() const { return n; }
-    AI int nout() const { return n; }
-    AI unsigned mask() const { return ((1u << n) - 1) | (((1u << n) - 1) << 9); }
-    AI void term(const Terms& T, int p, double* v) const { T.coef(p, v); }
+    AI unsigned mask() const { return (1u << NR) - 1; }
+    AI void term(const Terms& T, int p, double* v) const {
+        double t[9];
+        T.coef(p, t);
+        UNR for (int e = 0; e < NN; e++) v[e] = t[e];
+    }
     AI bool group(const double* s, double* out, double* red) const {
-        const bool keep = frob_norm(s, n) > thr;
-        UNR for (int e = 0; e < 9; e++) {
-            if (e < n) {
-                if (keep) { out[e] = s[e]; red[9 + e] = red[9 + e] + fabs(s[e]); }
-                else red[e] = red[e] + fabs(s[e]);
-            }
+        const bool keep = frob_norm(s, NN) > thr;
+        UNR for (int e = 0; e < NN; e++) {
+            if (keep) { out[e] = s[e]; red[NN + e] = red[NN + e] + fabs(s[e]); }
+            else red[e] = red[e] + fabs(s[e]);
         }
         return keep;
     }
-    AI void finish(Ctx& x, int o, const double* red) const { finish_t0(x, x.H[o], red, red + 9, n); }
+    AI void finish(Ctx& x, int o, const double* red) const { finish_t0(x, x.H[o], red, red + NN, NN); }
 };
 
 // fused PZ x PZ cross product of two 3x1 PZs a, b (PZsparse.cu:1118-1167 composes it from element
@@ -520,13 +523,12 @@ struct PolBlock {
 // every intermediate prune is replicated per hash group.
 struct PolCrossPP {
     static constexpr int NV = 6;
+    static constexpr int NO = 3;
     static constexpr int NR = 15;   // [0,6) product prunes, [6,9) difference prunes, [9,12) stack prunes, [12,15) absum
     double thr;
     const double* ac;               // operand centres (LDS handles)
     const double* bc;
     int a, b;                       // operand handle slots
-    AI int nv() const { return 6; }
-    AI int nout() const { return 3; }
     AI unsigned mask() const { return (1u << NR) - 1; }
     AI static void prods(const double* u, const double* w, double* v) {
         v[0] = u[1] * w[2]; v[1] = u[2] * w[1]; v[2] = u[2] * w[0];
@@ -547,7 +549,6 @@ struct PolCrossPP {
             T.S[1].read(q % nb, false, w);
         }
         prods(u, w, v);
-        UNR for (int e = 6; e < 9; e++) v[e] = 0.0;
     }
     AI bool group(const double* s, double* out, double* red) const {
         bool pres[6];
@@ -640,19 +641,18 @@ AI void block_sum_mask(const Ctx& x, double* v, int nr, unsigned mask) {
     }
 template <class Pol>
 __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
-    constexpr int NV = Pol::NV;
-    const int nv = pol.nv(), n = pol.nout();
+    constexpr int NV = Pol::NV, n = Pol::NO;
     const int lane = x.g.tid & 63;
     long long ph_t = x.phase ? clock64() : 0;
     uint64_t h = ~(uint64_t)0;
-    double c[9];
+    double c[NV];
     if (lane < N) {
         h = T.hash(lane);
         pol.term(T, lane, c);
     } else {
-        UNR for (int e = 0; e < 9; e++) c[e] = 0.0;
+        UNR for (int e = 0; e < NV; e++) c[e] = 0.0;
     }
-    if (x.phase) { UNR for (int e = 0; e < 9; e++) h ^= (c[e] != c[e]) ? 1 : 0; }  // force the loads before the stamp
+    if (x.phase) { UNR for (int e = 0; e < NV; e++) h ^= (c[e] != c[e]) ? 1 : 0; }  // force the loads before the stamp
     SPHASE(8)
     uint32_t id = (uint32_t)lane;
     int P = 1;
@@ -671,7 +671,7 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     }
     SPHASE(9)
     // term values follow their keys
-    UNR for (int e = 0; e < NV; e++) if (e < nv) c[e] = __shfl(c[e], (int)id, 64);
+    UNR for (int e = 0; e < NV; e++) c[e] = __shfl(c[e], (int)id, 64);
     const uint64_t prev = prev_u64(h);
     const bool head = lane < N && (lane == 0 || h != prev);
     const unsigned long long hm = __ballot(head);
@@ -679,17 +679,17 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     const int next = above ? __builtin_ctzll(above) : N;
     const int size = head ? next - lane : 0;
     const int maxg = wave_max(size);
-    double acc[9], t[9];
-    UNR for (int e = 0; e < 9; e++) { acc[e] = c[e]; t[e] = c[e]; }
+    double acc[NV], t[NV];
+    UNR for (int e = 0; e < NV; e++) { acc[e] = c[e]; t[e] = c[e]; }
     for (int st = 1; st < maxg; st++) {
         // t <- value of lane + 1: after st shifts lane q holds the term at q + st
-        UNR for (int e = 0; e < NV; e++) if (e < nv) t[e] = next_f64(t[e]);
-        if (head && st < size) UNR for (int e = 0; e < NV; e++) if (e < nv) acc[e] = acc[e] + t[e];
+        UNR for (int e = 0; e < NV; e++) t[e] = next_f64(t[e]);
+        if (head && st < size) UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + t[e];
     }
     SPHASE(10)
-    double red[Pol::NR], out[9];
+    double red[Pol::NR], out[n];
     UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
-    UNR for (int e = 0; e < 9; e++) out[e] = 0.0;
+    UNR for (int e = 0; e < n; e++) out[e] = 0.0;
     const bool keep = head && pol.group(acc, out, red);
     if (!head) UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
     const unsigned long long km = __ballot(keep);
@@ -711,7 +711,7 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     if (ok && keep) {
         x.A->h[hoff + pos] = h;
         double* dst = x.A->c + coff + (long)pos * n;
-        UNR for (int e = 0; e < 9; e++) if (e < n) dst[e] = out[e];
+        UNR for (int e = 0; e < n; e++) dst[e] = out[e];
     }
     SPHASE(11)
     const unsigned mask = pol.mask();
@@ -781,39 +781,28 @@ __device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const 
 }
 #endif
 
-#if defined(__HIP_DEVICE_COMPILE__)
-#define PHASE(k)                                                                                   \
-    if (x.phase && g.tid == 0) {                                                                   \
-        const long long c_ = clock64();                                                            \
-        x.phase[k] += (unsigned long long)(c_ - ph_t);                                             \
-        ph_t = c_;                                                                                 \
-    }
-#else
-#define PHASE(k)
-#endif
 
-// ---- N > 64: whole group. Output header initialised and sources staged (caller's barrier done).
-template <class Pol>
-AI void simplify_big(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
+
+// ---- N > 64: whole group. Key order first (independent of the policy), then the group passes.
+// Keys live in LDS up to its capacity, else in the workgroup's global buffers. Returns false (and
+// flags the error) when even those are too small. Sources staged, caller's barrier done.
+struct KeyBufs {
+    uint64_t* kh;
+    uint32_t* ki;
+    int* kp;
+};
+AI bool order_keys(Ctx& x, const Terms& T, int N, KeyBufs& K) {
     const Grp& g = x.g;
-#if defined(__HIP_DEVICE_COMPILE__)
-    long long ph_t = x.phase ? clock64() : 0;
-#endif
-    constexpr int NV = Pol::NV;
-    const int nv = pol.nv(), n = pol.nout();
-    uint64_t* kh = x.kh;
-    uint32_t* ki = x.ki;
-    int* kp = x.kp;
+    K.kh = x.kh; K.ki = x.ki; K.kp = x.kp;
     const bool in_lds = N <= x.cap_lds;
     if (!in_lds) {
-        kh = x.gkh; ki = x.gki; kp = x.gkp;
+        K.kh = x.gkh; K.ki = x.gki; K.kp = x.gkp;
         int P = 1;
         while (P < N) P <<= 1;
-        if (P > x.cap_glb) {
-            if (g.tid == 0) { *x.err |= ERR_SORTCAP; x.H[o].cnt = 0; }
-            return;
-        }
+        if (P > x.cap_glb) return false;
     }
+    uint64_t* kh = K.kh;
+    uint32_t* ki = K.ki;
     // order the keys: rank merge of sorted runs, or a sort
     bool rank_ok = T.runs() <= 6 || (x.mode & 2);
 #if !defined(__HIP_DEVICE_COMPILE__)
@@ -842,7 +831,7 @@ AI void simplify_big(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
     }
 #endif
     else {
-        // many runs and beyond the LDS key capacity: bitonic in global memory
+        // many runs and beyond the register sort: bitonic in global memory
         int P = 1;
         while (P < N) P <<= 1;
         for (int q = g.tid; q < P; q += g.n) {
@@ -853,11 +842,34 @@ AI void simplify_big(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
         bitonic_mem(x, kh, ki, P);
     }
     g.sync();
-    PHASE(1)
-    // group sums in term order, keep flags, pruned amounts
-    double red[Pol::NR], acc[9], tmp[9], out[9];
+    return true;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PHASE(k)                                                                                   \
+    if (x.phase && g.tid == 0) {                                                                   \
+        const long long c_ = clock64();                                                            \
+        x.phase[k] += (unsigned long long)(c_ - ph_t);                                             \
+        ph_t = c_;                                                                                 \
+    }
+#else
+#define PHASE(k)
+#endif
+
+// group sums in term order, keep flags and pruned amounts, compaction, output (keys ordered)
+template <class Pol>
+AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, const KeyBufs& K) {
+    const Grp& g = x.g;
+#if defined(__HIP_DEVICE_COMPILE__)
+    long long ph_t = x.phase ? clock64() : 0;
+#endif
+    constexpr int NV = Pol::NV, n = Pol::NO;
+    const uint64_t* kh = K.kh;
+    const uint32_t* ki = K.ki;
+    int* kp = K.kp;
+    double red[Pol::NR], acc[NV], tmp[NV], out[n];
     UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
-    UNR for (int e = 0; e < 9; e++) out[e] = 0.0;
+    UNR for (int e = 0; e < n; e++) out[e] = 0.0;
     for (int q = g.tid; q < N; q += g.n) {
         const bool head = q == 0 || kh[q] != kh[q - 1];
         int keep = 0;
@@ -865,7 +877,7 @@ AI void simplify_big(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
             pol.term(T, ki[q], acc);
             for (int r = q + 1; r < N && kh[r] == kh[q]; r++) {
                 pol.term(T, ki[r], tmp);
-                UNR for (int e = 0; e < NV; e++) if (e < nv) acc[e] = acc[e] + tmp[e];
+                UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + tmp[e];
             }
             keep = pol.group(acc, out, red) ? 1 : 0;
         }
@@ -873,32 +885,32 @@ AI void simplify_big(Ctx& x, int o, const Terms& T, const Pol& pol, int N) {
     }
     g.sync();
     PHASE(2)
-    const int K = block_scan(x, kp, N);
+    const int K_ = block_scan(x, kp, N);
     if (g.tid == 0) {
-        arena_alloc_t0(x, x.H[o], K, n);
-        x.A->bytes += T.in_bytes() + (double)K * (8.0 + 8.0 * n);
+        arena_alloc_t0(x, x.H[o], K_, n);
+        x.A->bytes += T.in_bytes() + (double)K_ * (8.0 + 8.0 * n);
     }
     g.sync();
     PHASE(3)
     const long hoff = x.H[o].hoff, coff = x.H[o].coff;
-    if (x.H[o].cnt == K) {
+    if (x.H[o].cnt == K_) {
         double dummy[Pol::NR];
         for (int q = g.tid; q < N; q += g.n) {
             const bool head = q == 0 || kh[q] != kh[q - 1];
             if (!head) continue;
-            const bool keep = (q + 1 < N) ? (kp[q + 1] != kp[q]) : (kp[q] != K);
+            const bool keep = (q + 1 < N) ? (kp[q + 1] != kp[q]) : (kp[q] != K_);
             if (!keep) continue;
             pol.term(T, ki[q], acc);
             for (int r = q + 1; r < N && kh[r] == kh[q]; r++) {
                 pol.term(T, ki[r], tmp);
-                UNR for (int e = 0; e < NV; e++) if (e < nv) acc[e] = acc[e] + tmp[e];
+                UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + tmp[e];
             }
             UNR for (int e = 0; e < Pol::NR; e++) dummy[e] = 0.0;
             pol.group(acc, out, dummy);
             const long pos = kp[q];
             x.A->h[hoff + pos] = kh[q];
             double* dst = x.A->c + coff + pos * n;
-            UNR for (int e = 0; e < 9; e++) if (e < n) dst[e] = out[e];
+            UNR for (int e = 0; e < n; e++) dst[e] = out[e];
         }
     }
     PHASE(4)

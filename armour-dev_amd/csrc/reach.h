@@ -515,46 +515,46 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                 cross_const(x, op.o, op.a, C);
                 break;
             }
-            case OP_CROSS_PP: {
-                Terms Tm;
-                terms_cross_pp(x, op.a, op.b, Tm);
-                const int N = op_terms(x, op);
-                PolCrossPP pol;
-                pol.thr = x.thr;
-                pol.ac = cen(x, x.H[op.a]);
-                pol.bc = cen(x, x.H[op.b]);
-                pol.a = op.a;
-                pol.b = op.b;
-                if (tid == 0) hdr_init(x, x.H[op.o], 3, 1);
-#if defined(__HIP_DEVICE_COMPILE__)
-                if (N <= 64 && !(x.mode & 1)) {
-                    if (tid < 64) simplify_small(x, op.o, Tm, pol, N);
-                    break;
-                }
-#endif
-                stage_sources(x, Tm);
-                x.g.sync();
-                simplify_big(x, op.o, Tm, pol, N);
-                break;
-            }
             default: {
-                // MUL / ADD / STACK3 / ADD1D: term list, header, simplify
+                // MUL / ADD / STACK3 / ADD1D / CROSS_PP: term list, header, simplify. The ordering of
+                // large term lists is shared; the group passes are instantiated per output class.
                 Terms Tm;
-                op_terms_of(x, op, Tm);
+                int cls;  // 0: 1x1, 1: 3x1, 2: 3x3 plain simplify, 3: fused PZ x PZ cross
+                if (op.code == OP_CROSS_PP) {
+                    terms_cross_pp(x, op.a, op.b, Tm);
+                    cls = 3;
+                } else {
+                    op_terms_of(x, op, Tm);
+                    cls = Tm.nout == 1 ? 0 : (Tm.nout == 3 ? 1 : 2);
+                }
                 const int N = op_terms(x, op);
 #if defined(__HIP_DEVICE_COMPILE__)
                 long long ph0 = (x.phase && tid == 0) ? clock64() : 0;
 #endif
-                if (tid == 0) op_header(x, op, Tm);
+                if (tid == 0) {
+                    if (cls == 3) hdr_init(x, x.H[op.o], 3, 1);
+                    else op_header(x, op, Tm);
+                }
 #if defined(__HIP_DEVICE_COMPILE__)
                 if (x.phase && tid == 0) x.phase[14] += (unsigned long long)(clock64() - ph0);
 #endif
-                PolBlock pol;
-                pol.n = Tm.nout;
-                pol.thr = x.thr;
+                PolBlock<1> p1{x.thr};
+                PolBlock<3> p3{x.thr};
+                PolBlock<9> p9{x.thr};
+                PolCrossPP pp;
+                pp.thr = x.thr;
+                pp.ac = cen(x, x.H[op.a]);
+                pp.bc = cen(x, x.H[op.b]);
+                pp.a = op.a;
+                pp.b = op.b;
 #if defined(__HIP_DEVICE_COMPILE__)
                 if (N <= 64 && !(x.mode & 1)) {
-                    if (tid < 64) simplify_small(x, op.o, Tm, pol, N);
+                    if (tid < 64) {
+                        if (cls == 0) simplify_small(x, op.o, Tm, p1, N);
+                        else if (cls == 1) simplify_small(x, op.o, Tm, p3, N);
+                        else if (cls == 2) simplify_small(x, op.o, Tm, p9, N);
+                        else simplify_small(x, op.o, Tm, pp, N);
+                    }
                     break;
                 }
                 long long pt = (x.phase && tid == 0) ? clock64() : 0;
@@ -562,9 +562,20 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                 stage_sources(x, Tm);
                 x.g.sync();
 #if defined(__HIP_DEVICE_COMPILE__)
-                if (x.phase && tid == 0) x.phase[6] += (unsigned long long)(clock64() - pt);
+                if (x.phase && tid == 0) { const long long c_ = clock64(); x.phase[6] += (unsigned long long)(c_ - pt); pt = c_; }
 #endif
-                simplify_big(x, op.o, Tm, pol, N);
+                KeyBufs K;
+                if (!order_keys(x, Tm, N, K)) {
+                    if (tid == 0) { *x.err |= ERR_SORTCAP; x.H[op.o].cnt = 0; }
+                    break;
+                }
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (x.phase && tid == 0) x.phase[1] += (unsigned long long)(clock64() - pt);
+#endif
+                if (cls == 0) simplify_groups(x, op.o, Tm, p1, N, K);
+                else if (cls == 1) simplify_groups(x, op.o, Tm, p3, N, K);
+                else if (cls == 2) simplify_groups(x, op.o, Tm, p9, N, K);
+                else simplify_groups(x, op.o, Tm, pp, N, K);
                 break;
             }
         }
