@@ -51,6 +51,7 @@ struct armour_planner {
     // reach program (ProgramBuilder::ops) on the device
     Op* d_prog = nullptr;
     int* d_slot_off = nullptr;
+    JrsJoint* d_jrs = nullptr;
     int nops = 0, nslots = 0;
     unsigned long long* d_bytes = nullptr;
     unsigned long long* d_prof = nullptr;  // per-op [cycles, terms] when ARMOUR_PROFILE_OPS is set
@@ -163,6 +164,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     }
     ra.arena_cap = 1 << 17;
     ra.gcap = 1 << 15;
+    if ((rc = p->alloc(&p->d_jrs, jobs * NF))) return rc;
     if ((rc = p->alloc(&ra.arena_h, (size_t)p->reach_grid * ra.arena_cap)) ||
         (rc = p->alloc(&ra.arena_c, (size_t)p->reach_grid * ra.arena_cap * 3)) ||
         (rc = p->alloc(&ra.gkh, (size_t)p->reach_grid * ra.gcap)) || (rc = p->alloc(&ra.gki, (size_t)p->reach_grid * ra.gcap)) ||
@@ -249,7 +251,11 @@ static int run_reach(armour_planner* p) {
     HIPCK(hipMemsetAsync(p->d_bytes, 0, sizeof(unsigned long long), p->stream));
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
+    const long nj = jobs * NF;
     HIPCK(hipEventRecord(p->ev[3], p->stream));
+    hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, p->stream, p->d_rp, p->W, p->T, p->q0, p->qd0,
+                       p->qdd0, p->d_jrs);
+    ra.jrs = p->d_jrs;
     hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, p->stream, p->d_rp, ra, p->ro);
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(p->ev[4], p->stream));

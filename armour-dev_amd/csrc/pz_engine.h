@@ -1145,6 +1145,113 @@ AI void header_mul(Ctx& x, int o, int a, int b, const Terms& T) {
     if (!as && !bs && !(A.R == 3 && A.C == 3 && B.R == 3)) *x.err |= ERR_HANDLES;  // block shape outside matmul()
 }
 
+// ---- element-parallel headers: lane e < R*C of wave 0 computes output element e (the same
+// arithmetic, element for element, as the serial formulas above); lane 0 also writes the meta.
+AI void set_meta(PZH& h, int R, int C) {
+    h.R = R; h.C = C; h.cnt = 0; h.stride = R * C; h.hoff = 0; h.coff = 0;
+    h.comp = -1; h.scaled = 0; h.scale = 1.0;
+}
+
+AI void header_add_par(Ctx& x, int o, int a, int b, int sign, int e) {
+    const PZH& A = x.H[a];
+    const PZH& B = x.H[b];
+    PZH& h = x.H[o];
+    const int n = nel(A);
+    if (e == 0) set_meta(h, A.R, A.C);
+    if (e >= n) return;
+    const double* pa = x.pool + A.off;
+    const double* pb = x.pool + B.off;
+    double* ph = x.pool + h.off;
+    ph[e] = sign > 0 ? pa[e] + pb[e] : pa[e] - pb[e];
+    ph[n + e] = pa[n + e] + pb[n + e];
+    ph[2 * n + e] = pa[2 * n + e] + pb[2 * n + e];
+    ph[3 * n + e] = 0.0;
+}
+
+AI void header_mul_par(Ctx& x, int o, int a, int b, int e) {
+    const PZH& A = x.H[a];
+    const PZH& B = x.H[b];
+    PZH& h = x.H[o];
+    const bool as = A.R == 1 && A.C == 1, bs = B.R == 1 && B.C == 1;
+    const int R = as ? B.R : A.R, C = as ? B.C : (bs ? A.C : B.C), nr = R * C;
+    const int na = nel(A), nb = nel(B);
+    if (e == 0) {
+        set_meta(h, R, C);
+        if (as && !bs && B.R != 1 && A.cnt > 0 && B.cnt > 0) *x.err |= ERR_HANDLES;  // Eigen assert in the reference
+        if (!as && !bs && !(A.R == 3 && A.C == 3 && B.R == 3)) *x.err |= ERR_HANDLES;  // block shape outside matmul()
+    }
+    if (e >= nr) return;
+    const double* Ac = x.pool + A.off;
+    const double* Bc = x.pool + B.off;
+    const double* Aa = Ac + 3 * na;
+    const double* Ba = Bc + 3 * nb;
+    double* ph = x.pool + h.off;
+    // centre (prod), then ind_v = A.ind B.ind + (|A.c| + sum|a_i|) B.ind + A.ind (|B.c| + sum|b_j|)
+    if (as) {
+        ph[e] = Ac[0] * Bc[e];
+        const double r2 = fabs(Ac[0]) + Aa[0], r3 = fabs(Bc[e]) + Ba[e];
+        UNR for (int v = 0; v < 2; v++) {
+            const double ai = Ac[(1 + v) * na], bi = Bc[(1 + v) * nb + e];
+            ph[(1 + v) * nr + e] = ai * bi + (r2 * bi + ai * r3);
+        }
+    } else if (bs) {
+        ph[e] = Ac[e] * Bc[0];
+        const double r2 = fabs(Ac[e]) + Aa[e], r3 = fabs(Bc[0]) + Ba[0];
+        UNR for (int v = 0; v < 2; v++) {
+            const double ai = Ac[(1 + v) * na + e], bi = Bc[(1 + v) * nb];
+            ph[(1 + v) * nr + e] = ai * bi + (r2 * bi + ai * r3);
+        }
+    } else {
+        // 3x3 times 3xC, column-major element (i, j), inner index summed in order (matmul())
+        const int i = e % 3, j = e / 3;
+        ph[e] = (Ac[i] * Bc[3 * j] + Ac[i + 3] * Bc[3 * j + 1]) + Ac[i + 6] * Bc[3 * j + 2];
+        double r2[3], r3[3];
+        UNR for (int k = 0; k < 3; k++) {
+            r2[k] = fabs(Ac[i + 3 * k]) + Aa[i + 3 * k];
+            r3[k] = fabs(Bc[k + 3 * j]) + Ba[k + 3 * j];
+        }
+        UNR for (int v = 0; v < 2; v++) {
+            const double* Ai = Ac + (1 + v) * na;
+            const double* Bi = Bc + (1 + v) * nb;
+            const double t2 = (r2[0] * Bi[3 * j] + r2[1] * Bi[3 * j + 1]) + r2[2] * Bi[3 * j + 2];
+            const double t3 = (Ai[i] * r3[0] + Ai[i + 3] * r3[1]) + Ai[i + 6] * r3[2];
+            const double ii = (Ai[i] * Bi[3 * j] + Ai[i + 3] * Bi[3 * j + 1]) + Ai[i + 6] * Bi[3 * j + 2];
+            ph[(1 + v) * nr + e] = ii + (t2 + t3);
+        }
+    }
+    ph[3 * nr + e] = 0.0;
+}
+
+AI void header_stack3_par(Ctx& x, int o, int a0, int a1, int a2, int e) {
+    PZH& h = x.H[o];
+    if (e == 0) set_meta(h, 3, 1);
+    if (e >= 3) return;
+    const PZH& S = x.H[e == 0 ? a0 : (e == 1 ? a1 : a2)];
+    const double* ps = x.pool + S.off;
+    double* ph = x.pool + h.off;
+    ph[e] = ps[0];
+    ph[3 + e] = ps[1];
+    ph[6 + e] = ps[2];
+    ph[9 + e] = 0.0;
+}
+
+AI void header_add_one_dim_par(Ctx& x, int o, int self, int a, int pos, int e) {
+    const PZH& A = x.H[self];
+    const PZH& B = x.H[a];
+    PZH& h = x.H[o];
+    const int n = nel(A);
+    if (e == 0) set_meta(h, A.R, A.C);
+    if (e >= n) return;
+    const double* pa = x.pool + A.off;
+    const double* pb = x.pool + B.off;
+    double* ph = x.pool + h.off;
+    const bool at = e == pos;
+    ph[e] = at ? pa[e] + pb[0] : pa[e];
+    ph[n + e] = at ? pa[n + e] + pb[1] : pa[n + e];
+    ph[2 * n + e] = at ? pa[2 * n + e] + pb[2] : pa[2 * n + e];
+    ph[3 * n + e] = 0.0;
+}
+
 // fused PZ x PZ cross: the term list of the six 1x1 products is the product term list of the two
 // full 3x1 operands (hashes only; PolCrossPP evaluates the coefficients)
 AI void terms_cross_pp(const Ctx& x, int a, int b, Terms& T) {

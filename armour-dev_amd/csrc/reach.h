@@ -449,6 +449,15 @@ AI void op_terms_of(const Ctx& x, const Op& op, Terms& T) {
         default: terms_add_one_dim(x, op.a, op.b, op.i, T); break;
     }
 }
+// output header, element-parallel: called by lanes e = 0..8 of wave 0
+AI void op_header_par(Ctx& x, const Op& op, int e) {
+    switch (op.code) {
+        case OP_MUL: header_mul_par(x, op.o, op.a, op.b, e); break;
+        case OP_ADD: header_add_par(x, op.o, op.a, op.b, op.i, e); break;
+        case OP_STACK3: header_stack3_par(x, op.o, op.a, op.b, op.c, e); break;
+        default: header_add_one_dim_par(x, op.o, op.a, op.b, op.i, e); break;
+    }
+}
 // output header (thread 0)
 AI void op_header(Ctx& x, const Op& op, const Terms& T) {
     switch (op.code) {
@@ -465,7 +474,7 @@ AI void op_header(Ctx& x, const Op& op, const Terms& T) {
 constexpr int DUMP_W = 8;
 AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int T, int t, const double* q0,
                     const double* qd0, const double* qdd0, const ReachOut& out, long j, JrsJoint* jrs,
-                    double* scratch, unsigned long long* prof, double* dump = nullptr) {
+                    double* scratch, unsigned long long* prof, double* dump = nullptr, const JrsJoint* jrs_in = nullptr) {
     const int tid = x.g.tid;
     double* rdist = scratch;
     double* ured = scratch + NF;
@@ -484,7 +493,13 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 #endif
         switch (op.code) {
             case OP_JRS:
-                for (int i = tid; i < NF; i += x.g.n) jrs[i] = jrs_joint(rp, T, t, i, q0[i], qd0[i], qdd0[i]);
+                // on the device the JRS scalars come from jrs_kernel (their interval arithmetic
+                // would otherwise set this kernel's register budget); the emulation computes them
+#if defined(__HIP_DEVICE_COMPILE__)
+                for (int i = tid; i < NF; i += x.g.n) jrs[i] = jrs_in[i];
+#else
+                for (int i = tid; i < NF; i += x.g.n) jrs[i] = jrs_in ? jrs_in[i] : jrs_joint(rp, T, t, i, q0[i], qd0[i], qdd0[i]);
+#endif
                 break;
             case OP_MAKE1D: if (tid == 0) t0_make_1d(x, op.o, jrs[op.i], op.i, op.b); break;
             case OP_MAKEROT: if (tid == 0) t0_make_rot(x, op.o, rp, jrs[op.i], op.i); break;
@@ -531,10 +546,15 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 #if defined(__HIP_DEVICE_COMPILE__)
                 long long ph0 = (x.phase && tid == 0) ? clock64() : 0;
 #endif
-                if (tid == 0) {
-                    if (cls == 3) hdr_init(x, x.H[op.o], 3, 1);
-                    else op_header(x, op, Tm);
+#if defined(__HIP_DEVICE_COMPILE__)
+                if (tid < 9) {
+                    if (cls == 3) { if (tid == 0) hdr_init(x, x.H[op.o], 3, 1); }
+                    else op_header_par(x, op, tid);
                 }
+#else
+                if (cls == 3) hdr_init(x, x.H[op.o], 3, 1);
+                else for (int e = 0; e < 9; e++) op_header_par(x, op, e);
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
                 if (x.phase && tid == 0) x.phase[14] += (unsigned long long)(clock64() - ph0);
 #endif

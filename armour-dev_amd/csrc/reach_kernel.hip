@@ -13,8 +13,21 @@ constexpr int KEY_CAP_LDS = 1024;
 constexpr int STAGE_DOUBLES = 1280;
 constexpr int POOL_DOUBLES = 1024;   // handle payloads (ProgramBuilder::slot_offsets)
 
+// JRS scalars of every (world, interval, joint) (KPR/Trajectory.cu:63-254), one thread each
+__global__ void jrs_kernel(const RobotParams* __restrict__ rpp, int W, int T, const double* q0, const double* qd0,
+                           const double* qdd0, JrsJoint* out) {
+    const long n = (long)W * T * NF;
+    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(idx % NF);
+        const long j = idx / NF;
+        const int t = (int)(j % T), w = (int)(j / T);
+        out[idx] = jrs_joint(*rpp, T, t, i, q0[w * NF + i], qd0[w * NF + i], qdd0[w * NF + i]);
+    }
+}
+
 struct ReachArgs {
     int W, T;
+    const JrsJoint* jrs;  // [W][T][NF] from jrs_kernel
     const double* q0;    // [W][NF]
     const double* qd0;
     const double* qdd0;
@@ -95,7 +108,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREA
         }
         __syncthreads();
         run_program(x, rp, a.prog, a.nops, a.T, t, q0s, qd0s, qdd0s, out, job, jrs, scratch, a.prof,
-                    job == 0 ? a.dump : nullptr);
+                    job == 0 ? a.dump : nullptr, a.jrs + job * NF);
         if (threadIdx.x == 0) {
             if (err) atomicOr(&out.err[w], err);
             atomicAdd(a.bytes, (unsigned long long)arena.bytes);
