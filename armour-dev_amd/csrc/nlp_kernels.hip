@@ -236,19 +236,33 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
     __syncthreads();
     if (!(d.diag & 1)) {
-        for (int i = tid; i < NJ * CAP_LM; i += blockDim.x) {
-            const int l = i / CAP_LM, q = i % CAP_LM;
-            if (q < lcnt[l]) {
+        // only the valid monomials, enumerated compactly (one load round per thread): u < L are
+        // link monomials, the rest torque monomials; prefix offsets from the per-PZ counts
+        int lpre[MAX_J + 1], tpre[NF + 1];
+        lpre[0] = 0;
+#pragma unroll
+        for (int l = 0; l < MAX_J; l++) lpre[l + 1] = lpre[l] + (l < NJ ? lcnt[l] : 0);
+        tpre[0] = 0;
+#pragma unroll
+        for (int j = 0; j < NF; j++) tpre[j + 1] = tpre[j] + tcnt[j];
+        const int L = lpre[MAX_J], M = tpre[NF];
+        for (int u = tid; u < L + M; u += blockDim.x) {
+            if (u < L) {
+                int l = 0, q0 = 0;
+#pragma unroll
+                for (int k = 1; k < MAX_J; k++) if (u >= lpre[k]) { l = k; q0 = lpre[k]; }
+                const int q = u - q0;
                 const long b = (jt * NJ + l) * CAP_LM + q;
                 lh[l][q] = d.ro.link_hash[b];
                 lco[l][q][0] = d.ro.link_coef[b * 3];
                 lco[l][q][1] = d.ro.link_coef[b * 3 + 1];
                 lco[l][q][2] = d.ro.link_coef[b * 3 + 2];
-            }
-        }
-        for (int i = tid; i < NF * CAP_UM; i += blockDim.x) {
-            const int j = i / CAP_UM, q = i % CAP_UM;
-            if (q < tcnt[j]) {
+            } else {
+                const int v = u - L;
+                int j = 0, q0 = 0;
+#pragma unroll
+                for (int k = 1; k < NF; k++) if (v >= tpre[k]) { j = k; q0 = tpre[k]; }
+                const int q = v - q0;
                 const long b = (jt * NF + j) * CAP_UM + q;
                 th[j][q] = d.ro.tq_hash[b];
                 tco[j][q] = d.ro.tq_coef[b];

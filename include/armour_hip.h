@@ -104,8 +104,8 @@ int armour_get_joint_bounds(const armour_planner* p, double* bounds28);
  * from the robot tables; these expose it for profiling. armour_get_reach_program writes the op
  * codes (if capacity >= count) and returns the op count. armour_get_reach_profile writes
  * [cycles, terms] per op accumulated over all jobs when the environment variable
- * ARMOUR_PROFILE_OPS was set at armour_create, followed by 8 phase counters of the large-operator
- * path (capacity counts pairs: >= op count + 4), and returns the op count. */
+ * ARMOUR_PROFILE_OPS was set at armour_create, followed by 16 phase counters of the operator
+ * paths (capacity counts pairs: >= op count + 8), and returns the op count. */
 int armour_get_reach_program(const armour_planner* p, int* codes, int capacity);
 int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms, int capacity);
 /* op-by-op state of job 0 (world 0, t = 0) of the last reach: per op 8 doubles [monomial count,
