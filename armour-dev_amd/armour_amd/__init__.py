@@ -15,7 +15,7 @@ from .robots import KINOVA
 from .worlds import csv_world, example_world, make_world, straight_line_waypoint
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libarmour_hip.so")
+LIB_PATH = os.environ.get("ARMOUR_LIB") or os.path.join(_HERE, "libarmour_hip.so")  # ARMOUR_LIB: diagnostics builds
 NF = 7
 _LIB = None
 _dp = ctypes.POINTER(ctypes.c_double)

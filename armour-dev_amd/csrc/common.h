@@ -17,6 +17,8 @@ constexpr int OBS_GEN = 3;     // MAX_OBSTACLE_GENERATOR_NUM
 constexpr int MAX_OBS = 40;    // MAX_OBSTACLE_NUM (KPR/Parameters.h:26)
 constexpr int BUF_GEN = OBS_GEN + 6;
 constexpr int COMB = BUF_GEN * (BUF_GEN - 1) / 2;  // 36 generator pairs
+constexpr int LL_PLANES = 15;  // planes spanned by two link generators (6 choose 2)
+constexpr int OO_PLANES = OBS_GEN * (OBS_GEN - 1) / 2;  // planes spanned by two obstacle generators
 
 // monomial hash layout (KPR/PZsparse.h:23-40): k (7 x 2 bit) | qde | qdae | qddae (7 x 1 bit) |
 // cosqe | sinqe (7 x 2 bit)

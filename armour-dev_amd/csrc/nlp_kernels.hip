@@ -57,6 +57,17 @@ __device__ inline double row_va(const NlpDev& d, int slot, int w, int r, const d
     return x[r - d.m];
 }
 
+// normalised cross product of a generator pair, zero for a parallel pair (CollisionChecking.cu:136-228)
+__device__ inline __attribute__((always_inline)) void plane_normal(const double* ga, const double* gb, double& C0,
+                                                                   double& C1, double& C2) {
+    const double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
+    const double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
+    const double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
+    const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
+    C0 = 0; C1 = 0; C2 = 0;
+    if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
+}
+
 // plane of the generator pair (ga, gb) (the arithmetic of buffered_plane below, pair given)
 __device__ inline __attribute__((always_inline)) void plane_of(const double* ga, const double* gb, const double (*G)[3],
                                                                const double* oc, double& C0, double& C1, double& C2,
@@ -225,9 +236,15 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     __shared__ double lgen[MAX_J][18];
     __shared__ double obs[MAX_OBS][12];
     __shared__ uint16_t lh[MAX_J][CAP_LM];
-    __shared__ double lco[MAX_J][CAP_LM][3];
     __shared__ uint16_t th[NF][CAP_UM];
-    __shared__ double tco[NF][CAP_UM];
+    // monomial coefficients while slicing; afterwards the same LDS holds the obstacle-independent
+    // link-link planes and the link-independent obstacle-obstacle planes
+    __shared__ double ubuf[MAX_J * CAP_LM * 3 + NF * CAP_UM];
+    auto lco = reinterpret_cast<double (*)[CAP_LM][3]>(ubuf);
+    auto tco = reinterpret_cast<double (*)[CAP_UM]>(ubuf + MAX_J * CAP_LM * 3);
+    static_assert(MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5 <= MAX_J * CAP_LM * 3 + NF * CAP_UM, "plane tables");
+    auto llp = reinterpret_cast<double (*)[LL_PLANES][10]>(ubuf);
+    auto oop = reinterpret_cast<double (*)[OO_PLANES][5]>(ubuf + MAX_J * LL_PLANES * 10);
     __shared__ int lcnt[MAX_J], tcnt[NF];
     if (tid < NF) x[tid] = mode == 1 ? S.xt[tid] : S.x[tid];
     if (tid < NJ) lcnt[tid] = d.ro.link_cnt[jt * NJ + tid];
@@ -365,11 +382,48 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         }
     }
     __syncthreads();
-    // collision rows (CollisionChecking.cu:230-299): one thread per (link, obstacle) scans the 36
-    // hyperplanes of the buffered obstacle in the reference's order (pos_p before neg_p, strict
-    // >), so the first maximum wins as in the reference's serial loop
+    // collision rows (CollisionChecking.cu:230-299). Of the 36 planes of a buffered obstacle, the
+    // 15 spanned by two link generators do not depend on the obstacle and the 3 spanned by two
+    // obstacle generators do not depend on the link: those are formed once per block, with the
+    // parts of d and delta they determine alone (delta's summands kept separate where the
+    // reference's left-to-right sum needs them in order), then the per-(link, obstacle) scan only
+    // completes them.
     const long nt = (long)NF * d.T;
-    for (int pr = tid; pr < ((d.diag & 2) ? 0 : NJ * O); pr += blockDim.x) {
+    const bool coll = !(d.diag & 2);
+    for (int u = tid; u < (coll ? NJ * LL_PLANES + O * OO_PLANES : 0); u += blockDim.x) {
+        if (u < NJ * LL_PLANES) {
+            const int l = u / LL_PLANES, p = u % LL_PLANES;
+            int i = 0, rem = p;
+            while (rem >= 5 - i) { rem -= 5 - i; i++; }
+            const int j = i + 1 + rem;
+            const double* ga = &lgen[l][3 * i];
+            const double* gb = &lgen[l][3 * j];
+            double A0, A1, A2;
+            plane_normal(ga, gb, A0, A1, A2);
+            double* P = llp[l][p];
+            P[0] = A0; P[1] = A1; P[2] = A2;
+            P[3] = A0 * lc[l][0] + A1 * lc[l][1] + A2 * lc[l][2];
+#pragma unroll
+            for (int k = 0; k < 6; k++) P[4 + k] = fabs(A0 * lgen[l][3 * k] + A1 * lgen[l][3 * k + 1] + A2 * lgen[l][3 * k + 2]);
+        } else {
+            const int v = u - NJ * LL_PLANES, o = v / OO_PLANES, p = v % OO_PLANES;
+            const int i = p == 2 ? 1 : 0, j = p == 0 ? 1 : 2;
+            double A0, A1, A2;
+            plane_normal(&obs[o][3 * (i + 1)], &obs[o][3 * (j + 1)], A0, A1, A2);
+            double* P = oop[o][p];
+            P[0] = A0; P[1] = A1; P[2] = A2;
+            P[3] = A0 * obs[o][0] + A1 * obs[o][1] + A2 * obs[o][2];
+            double del = 0.0;
+#pragma unroll
+            for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * obs[o][3 * (k + 1)] + A1 * obs[o][3 * (k + 1) + 1] + A2 * obs[o][3 * (k + 1) + 2]);
+            P[4] = del;
+        }
+    }
+    __syncthreads();
+    // one thread per (link, obstacle) scans the 36 planes in the reference's order (pairs (a, b),
+    // a < b, lexicographic: CollisionChecking.cu:26-39; pos_p before neg_p, strict >), so the first
+    // maximum wins as in the reference's serial loop
+    for (int pr = tid; pr < (coll ? NJ * O : 0); pr += blockDim.x) {
         const int l = pr / O, o = pr % O;
         double best = -100000000.0;
         double B0 = 0, B1 = 0, B2 = 0;
@@ -387,16 +441,34 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         for (int i = 0; i < 6; i++)
 #pragma unroll
             for (int r = 0; r < 3; r++) G[OBS_GEN + i][r] = lgen[l][r + 3 * i];
-        // pairs (a, b), a < b, lexicographic = the pair table's order (CollisionChecking.cu:26-39)
 #pragma unroll
         for (int a = 0; a < BUF_GEN; a++)
 #pragma unroll
             for (int b = a + 1; b < BUF_GEN; b++) {
-                double A0, A1, A2, dd, del;
-                plane_of(G[a], G[b], G, oc, A0, A1, A2, dd, del);
-                const double nrm = sqrt(A0 * A0 + A1 * A1 + A2 * A2);
-                if (nrm > 0) {
-                    const double Ac = A0 * c0 + A1 * c1 + A2 * c2;
+                double A0, A1, A2, dd, del, Ac;
+                if (b < OBS_GEN) {
+                    const double* P = oop[o][a + b - 1];
+                    A0 = P[0]; A1 = P[1]; A2 = P[2]; dd = P[3]; del = P[4];
+#pragma unroll
+                    for (int k = OBS_GEN; k < BUF_GEN; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
+                    Ac = A0 * c0 + A1 * c1 + A2 * c2;
+                } else if (a >= OBS_GEN) {
+                    const int i = a - OBS_GEN, j = b - OBS_GEN;
+                    const double* P = llp[l][i * (11 - i) / 2 + j - i - 1];
+                    A0 = P[0]; A1 = P[1]; A2 = P[2]; Ac = P[3];
+                    dd = A0 * oc[0] + A1 * oc[1] + A2 * oc[2];
+                    del = 0.0;
+#pragma unroll
+                    for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
+#pragma unroll
+                    for (int k = 0; k < 6; k++) del += P[4 + k];
+                } else {
+                    plane_of(G[a], G[b], G, oc, A0, A1, A2, dd, del);
+                    Ac = A0 * c0 + A1 * c1 + A2 * c2;
+                }
+                // the reference skips a zero normal (norm > 0); for a normalised or zeroed A
+                // that is exactly "some component non-zero"
+                if (A0 != 0 || A1 != 0 || A2 != 0) {
                     const double pos = Ac - (dd + del);
                     const double neg = -Ac - (-dd + del);
                     if (pos > best) { best = pos; B0 = A0; B1 = A1; B2 = A2; isneg = false; }

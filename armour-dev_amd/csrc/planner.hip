@@ -144,7 +144,12 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
         }
     }
     // reach workspace: four resident workgroups per CU, each with a private arena
-    p->reach_grid = 4 * p->ncu;
+    {
+        // ARMOUR_REACH_WG_PER_CU (diagnostics): fewer resident workgroups per CU than the 4 that fit
+        const char* wg = std::getenv("ARMOUR_REACH_WG_PER_CU");
+        const int per = wg ? std::atoi(wg) : REACH_WG_PER_CU;
+        p->reach_grid = (per >= 1 && per <= REACH_WG_PER_CU ? per : REACH_WG_PER_CU) * p->ncu;
+    }
     ReachArgs& ra = p->ra;
     ra.prog = p->d_prog;
     ra.nops = p->nops;

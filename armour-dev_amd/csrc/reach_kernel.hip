@@ -8,9 +8,16 @@
 
 namespace armour {
 
-constexpr int REACH_THREADS = 128;   // two waves per job, four jobs resident per CU
-constexpr int KEY_CAP_LDS = 1024;
-constexpr int STAGE_DOUBLES = 1280;
+#ifndef REACH_CFG_THREADS
+#define REACH_CFG_THREADS 128
+#define REACH_CFG_KEYS 1024
+#define REACH_CFG_STAGE 1280
+#define REACH_CFG_WG_PER_CU 4
+#endif
+constexpr int REACH_THREADS = REACH_CFG_THREADS;   // two waves per job, four jobs resident per CU
+constexpr int KEY_CAP_LDS = REACH_CFG_KEYS;
+constexpr int STAGE_DOUBLES = REACH_CFG_STAGE;
+constexpr int REACH_WG_PER_CU = REACH_CFG_WG_PER_CU;
 constexpr int POOL_DOUBLES = 1024;   // handle payloads (ProgramBuilder::slot_offsets)
 
 // JRS scalars of every (world, interval, joint) (KPR/Trajectory.cu:63-254), one thread each
