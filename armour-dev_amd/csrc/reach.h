@@ -472,6 +472,10 @@ AI void op_header(Ctx& x, const Op& op, const Terms& T) {
 // dump (diagnostics, may be null): per op, the output handle's [cnt, R*C, centre[0..2], ind0[0],
 // ind1[0], absum[0]] after the op
 constexpr int DUMP_W = 8;
+#if !defined(__HIP_DEVICE_COMPILE__)
+// host emulation statistics (tests/emu): per op [code, class, term kind, |S0|, |S1|, N, runs, output count]
+inline int* g_op_stats = nullptr;
+#endif
 AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int T, int t, const double* q0,
                     const double* qd0, const double* qdd0, const ReachOut& out, long j, JrsJoint* jrs,
                     double* scratch, unsigned long long* prof, double* dump = nullptr, const JrsJoint* jrs_in = nullptr) {
@@ -543,6 +547,13 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                     cls = Tm.nout == 1 ? 0 : (Tm.nout == 3 ? 1 : 2);
                 }
                 const int N = op_terms(x, op);
+#if !defined(__HIP_DEVICE_COMPILE__)
+                if (g_op_stats) {
+                    int* st = g_op_stats + 8 * pc;
+                    st[0] = op.code; st[1] = cls; st[2] = Tm.kind; st[3] = Tm.S[0].cnt;
+                    st[4] = Tm.ns > 1 ? Tm.S[1].cnt : 0; st[5] = N; st[6] = Tm.runs();
+                }
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
                 long long ph0 = (x.phase && tid == 0) ? clock64() : 0;
 #endif
@@ -600,6 +611,9 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
             }
         }
         if (op.sync) x.g.sync();
+#if !defined(__HIP_DEVICE_COMPILE__)
+        if (g_op_stats && op.o >= 0) g_op_stats[8 * pc + 7] = x.H[op.o].cnt;
+#endif
         if (dump && op.o >= 0) {
             x.g.sync();
             if (tid == 0) {
