@@ -86,22 +86,17 @@ __device__ inline __attribute__((always_inline)) void plane_of(const double* ga,
 
 // one monomial's contribution to a slice (k = 0) or to its derivative in x_{k-1}: the products
 // of PZsparse.cu:404-435 / 477-516 in factor order, v * 1.0 standing in for a skipped factor
-__device__ inline __attribute__((always_inline)) double sel4(const double* t, int g) {
-    return g == 0 ? t[0] : (g == 1 ? t[1] : (g == 2 ? t[2] : t[3]));
-}
-__device__ inline __attribute__((always_inline)) double slice_term(double co, int h, int k, const double (*pw)[4],
-                                                                   const double (*dpw)[4]) {
+// ptab[j][g] = x_j^g (g = 0: 1.0, the skipped factor exactly), ptab[j][4 + g] = g x_j^(g-1): one
+// LDS read per factor instead of a select chain (eval_kernel is VALU-issue bound)
+__device__ inline __attribute__((always_inline)) double slice_term(double co, int h, int k, const double (*ptab)[8]) {
     double v = co;
     bool zero = false;
 #pragma unroll
     for (int j = 0; j < NF; j++) {
         const int g = (h >> (2 * j)) & 3;
-        if (j == k - 1) {
-            zero = zero || g == 0;
-            v = v * sel4(dpw[j], g);
-        } else {
-            v = v * sel4(pw[j], g);
-        }
+        const bool dj = j == k - 1;
+        zero = zero || (dj && g == 0);
+        v = v * ptab[j][g + (dj ? 4 : 0)];
     }
     return zero ? 0.0 : v;
 }
@@ -246,7 +241,13 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     auto llp = reinterpret_cast<double (*)[LL_PLANES][10]>(ubuf);
     auto oop = reinterpret_cast<double (*)[OO_PLANES][5]>(ubuf + MAX_J * LL_PLANES * 10);
     __shared__ int lcnt[MAX_J], tcnt[NF];
-    if (tid < NF) x[tid] = mode == 1 ? S.xt[tid] : S.x[tid];
+    __shared__ double ptab[NF][8];
+    if (tid < NF) {
+        const double xj = mode == 1 ? S.xt[tid] : S.x[tid];
+        x[tid] = xj;
+        ptab[tid][0] = 1.0; ptab[tid][1] = xj; ptab[tid][2] = xj * xj; ptab[tid][3] = xj * xj * xj;
+        ptab[tid][4] = 0.0; ptab[tid][5] = 1.0 * 1.0; ptab[tid][6] = 2.0 * xj; ptab[tid][7] = 3.0 * (xj * xj);
+    }
     if (tid < NJ) lcnt[tid] = d.ro.link_cnt[jt * NJ + tid];
     if (tid >= 32 && tid < 32 + NF) tcnt[tid - 32] = d.ro.tq_cnt[jt * NF + tid - 32];
     for (int i = tid; i < NJ * 18; i += blockDim.x) lgen[i / 18][i % 18] = d.ro.link_gens[jt * NJ * 18 + i];
@@ -289,15 +290,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     __syncthreads();
     // slices (PZsparse.cu:404-435 value, :477-516 gradient): one thread per output — k = 0 the
     // value, k = 1..7 the derivative in x_{k-1} — summing its terms in monomial order. Powers come
-    // from per-variable tables, selected without branches: pw[j][g] = x_j^g (g = 0: 1, factor
-    // skipped exactly), dpw[j][g] = g x_j^(g-1), the very products ipow forms.
-    double pw[NF][4], dpw[NF][4];
-#pragma unroll
-    for (int j = 0; j < NF; j++) {
-        const double xj = x[j];
-        pw[j][0] = 1.0; pw[j][1] = xj; pw[j][2] = xj * xj; pw[j][3] = xj * xj * xj;
-        dpw[j][0] = 0.0; dpw[j][1] = 1.0 * 1.0; dpw[j][2] = 2.0 * xj; dpw[j][3] = 3.0 * (xj * xj);
-    }
+    // from a per-variable table (ptab, filled with the staging), the very products ipow forms.
     const int nlk = NJ * 3 * 8;
     for (int u = tid; u < ((d.diag & 1) ? 0 : nlk + NF * 8); u += blockDim.x) {
       if (u < nlk) {
@@ -307,7 +300,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         const int cnt = lcnt[l];
         for (int q = 0; q < cnt; q++) {
             const int h = lh[l][q];
-            c = c + slice_term(lco[l][q][e], h, k, pw, dpw);
+            c = c + slice_term(lco[l][q][e], h, k, ptab);
         }
         if (k == 0) {
             const double r = d.ro.link_rad[base * 3 + e];
@@ -323,7 +316,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         const long base = jt * NF + j;
         double c = k == 0 ? d.ro.tq_center[base] : 0.0;
         const int cnt = tcnt[j];
-        for (int q = 0; q < cnt; q++) c = c + slice_term(tco[j][q], th[j][q], k, pw, dpw);
+        for (int q = 0; q < cnt; q++) c = c + slice_term(tco[j][q], th[j][q], k, ptab);
         const long gi = gidx(d, slot, w, (long)t * NF + j);
         if (k == 0) {
             const double r = d.ro.tq_rad[base];
