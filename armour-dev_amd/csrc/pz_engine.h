@@ -83,6 +83,8 @@ struct Ctx {
     uint32_t* gki;
     int* gkp;
     int cap_glb;
+    double* gout;      // kept group values of the simplify in flight, by key position (HBM)
+    int gout_cap;      // doubles
     double* stage;     // operand staging (LDS), stage_cap doubles
     int stage_cap;
     double* red;       // reduction scratch (LDS): [waves * 18] on device, [n * 18] in the emulation
@@ -870,6 +872,9 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
     double red[Pol::NR], acc[NV], tmp[NV], out[n];
     UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
     UNR for (int e = 0; e < n; e++) out[e] = 0.0;
+    // the kept groups' values wait in gout for the compaction pass (same thread, same q), which
+    // then copies instead of summing the group again; without room it recomputes them
+    const bool cache = x.gout && (long)N * n <= x.gout_cap;
     for (int q = g.tid; q < N; q += g.n) {
         const bool head = q == 0 || kh[q] != kh[q - 1];
         int keep = 0;
@@ -880,6 +885,7 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
                 UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + tmp[e];
             }
             keep = pol.group(acc, out, red) ? 1 : 0;
+            if (keep && cache) UNR for (int e = 0; e < n; e++) x.gout[(long)q * n + e] = out[e];
         }
         kp[q] = keep;
     }
@@ -900,13 +906,17 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
             if (!head) continue;
             const bool keep = (q + 1 < N) ? (kp[q + 1] != kp[q]) : (kp[q] != K_);
             if (!keep) continue;
-            pol.term(T, ki[q], acc);
-            for (int r = q + 1; r < N && kh[r] == kh[q]; r++) {
-                pol.term(T, ki[r], tmp);
-                UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + tmp[e];
+            if (cache) {
+                UNR for (int e = 0; e < n; e++) out[e] = x.gout[(long)q * n + e];
+            } else {
+                pol.term(T, ki[q], acc);
+                for (int r = q + 1; r < N && kh[r] == kh[q]; r++) {
+                    pol.term(T, ki[r], tmp);
+                    UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + tmp[e];
+                }
+                UNR for (int e = 0; e < Pol::NR; e++) dummy[e] = 0.0;
+                pol.group(acc, out, dummy);
             }
-            UNR for (int e = 0; e < Pol::NR; e++) dummy[e] = 0.0;
-            pol.group(acc, out, dummy);
             const long pos = kp[q];
             x.A->h[hoff + pos] = kh[q];
             double* dst = x.A->c + coff + pos * n;
