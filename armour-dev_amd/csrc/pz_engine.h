@@ -314,6 +314,17 @@ struct Terms {
     const double* Bc;
     int AR, AC, BC;
     int nout;          // elements of the output block
+    uint32_t nbm;      // product: ceil(2^32 / |S1|), so T3 index q splits as q / nb = mulhi(q, nbm)
+    // T3 index q -> (row i, column j) without an integer division: exact for q, nb < 2^16
+    AI void split(int q, int& i, int& j) const {
+        const int nb = S[1].cnt;
+#if defined(__HIP_DEVICE_COMPILE__)
+        i = nb == 1 ? q : (int)__umulhi((uint32_t)q, nbm);
+#else
+        i = nb == 1 ? q : (int)(((uint64_t)(uint32_t)q * nbm) >> 32);
+#endif
+        j = q - i * nb;
+    }
     AI void which(int p, int& s, int& k) const {
         s = 0;
         if (p >= S[0].cnt) { p -= S[0].cnt; s = 1; if (p >= S[1].cnt) { p -= S[1].cnt; s = 2; } }
@@ -324,8 +335,9 @@ struct Terms {
             const int na = S[0].cnt, nb = S[1].cnt;
             if (p < na) return S[0].hash(p);
             if (p < na + nb) return S[1].hash(p - na);
-            const int q = p - na - nb;
-            return S[0].hash(q / nb) + S[1].hash(q % nb);
+            int i, j;
+            split(p - na - nb, i, j);
+            return S[0].hash(i) + S[1].hash(j);
         }
         int s, k;
         which(p, s, k);
@@ -353,9 +365,10 @@ struct Terms {
                 prod(a, b, out);
                 return;
             }
-            const int q = p - na - nb;
-            S[0].read(q / nb, false, a);
-            S[1].read(q % nb, false, b);
+            int i, j;
+            split(p - na - nb, i, j);
+            S[0].read(i, false, a);
+            S[1].read(j, false, b);
             prod(a, b, out);
             return;
         }
@@ -546,9 +559,10 @@ struct PolCrossPP {
             UNR for (int e = 0; e < 3; e++) u[e] = ac[e];
             T.S[1].read(p - na, false, w);
         } else {
-            const int q = p - na - nb;
-            T.S[0].read(q / nb, false, u);
-            T.S[1].read(q % nb, false, w);
+            int i, j;
+            T.split(p - na - nb, i, j);
+            T.S[0].read(i, false, u);
+            T.S[1].read(j, false, w);
         }
         prods(u, w, v);
     }
@@ -1116,6 +1130,7 @@ AI void terms_mul(const Ctx& x, int a, int b, Terms& T) {
     T.S[0] = src_of(x, A); T.S[1] = src_of(x, B);
     T.Ac = cen(x, A); T.Bc = cen(x, B);
     T.AR = A.R; T.AC = A.C; T.BC = B.C;
+    T.nbm = B.cnt > 1 ? 0xFFFFFFFFu / (uint32_t)B.cnt + 1u : 0u;
     const bool as = A.R == 1 && A.C == 1, bs = B.R == 1 && B.C == 1;
     T.nout = as ? nel(B) : (bs ? nel(A) : A.R * B.C);
 }
@@ -1272,6 +1287,7 @@ AI void terms_cross_pp(const Ctx& x, int a, int b, Terms& T) {
     T.S[0] = src_of(x, A); T.S[1] = src_of(x, B);
     T.Ac = cen(x, A); T.Bc = cen(x, B);
     T.AR = 3; T.AC = 1; T.BC = 1;
+    T.nbm = B.cnt > 1 ? 0xFFFFFFFFu / (uint32_t)B.cnt + 1u : 0u;
     T.nout = 3;
 }
 
