@@ -455,13 +455,25 @@ AI void stage_sources(Ctx& x, Terms& T) {
         Src& S = T.S[s];
         uint64_t* hs = (uint64_t*)base;
         double* cs = base + S.cnt;
-        for (int k = x.g.tid; k < S.cnt; k += x.g.n) {
-            hs[k] = S.h[k];
-            const double* src = S.c + (long)k * S.stride;
-            for (int e = 0; e < S.n; e++) {
-                double v = src[S.comp >= 0 ? S.comp : e];
-                if (S.scaled) v = S.scale * v;
-                cs[k * S.n + e] = v;
+        // two monomials per thread per round, every load of a round issued before its stores
+        for (int k = x.g.tid; k < S.cnt; k += 2 * x.g.n) {
+            const int k2 = k + x.g.n;
+            const bool two = k2 < S.cnt;
+            const uint64_t h1 = S.h[k], h2 = S.h[two ? k2 : k];
+            double v1[9], v2[9];
+            const double* s1 = S.c + (long)k * S.stride;
+            const double* s2 = S.c + (long)(two ? k2 : k) * S.stride;
+            UNR for (int e = 0; e < 9; e++) {
+                if (e < S.n) {
+                    v1[e] = s1[S.comp >= 0 ? S.comp : e];
+                    v2[e] = s2[S.comp >= 0 ? S.comp : e];
+                }
+            }
+            hs[k] = h1;
+            UNR for (int e = 0; e < 9; e++) if (e < S.n) cs[k * S.n + e] = S.scaled ? S.scale * v1[e] : v1[e];
+            if (two) {
+                hs[k2] = h2;
+                UNR for (int e = 0; e < 9; e++) if (e < S.n) cs[k2 * S.n + e] = S.scaled ? S.scale * v2[e] : v2[e];
             }
         }
         S.h = hs;
