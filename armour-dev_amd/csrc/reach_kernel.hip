@@ -14,6 +14,9 @@ namespace armour {
 #define REACH_CFG_STAGE 1280
 #define REACH_CFG_WG_PER_CU 4
 #endif
+#ifndef REACH_CFG_WAVES_PER_SIMD
+#define REACH_CFG_WAVES_PER_SIMD 2
+#endif
 constexpr int REACH_THREADS = REACH_CFG_THREADS;   // two waves per job, four jobs resident per CU
 constexpr int KEY_CAP_LDS = REACH_CFG_KEYS;
 constexpr int STAGE_DOUBLES = REACH_CFG_STAGE;
@@ -59,7 +62,7 @@ struct ReachArgs {
 };
 
 // 2 waves per SIMD: 256 registers per lane (VGPR + AGPR), four 2-wave workgroups per CU
-__global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREADS), amdgpu_waves_per_eu(2, 2))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
+__global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREADS), amdgpu_waves_per_eu(REACH_CFG_WAVES_PER_SIMD, REACH_CFG_WAVES_PER_SIMD))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
     __shared__ PZH H[MAX_SLOTS];
     __shared__ double pool[POOL_DOUBLES + 9];  // + 9: header reads of a full 3x3 past a small slot
     __shared__ uint64_t kh[KEY_CAP_LDS];
