@@ -1,13 +1,7 @@
-# one GPU call: GPU tests, smoke, bench line, rocprofv3 kernel trace of the bench
+# round-end evidence: GPU tests, smoke, bench (stdout JSON line) into gpurun_out/
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 900 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && \
+timeout -k 10 900 python3 -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 400 python3 bench.py > gpurun_out/bench.log 2>&1 && \
-cd /tmp && export TMPDIR=/tmp && \
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --cpu-seconds 0 > $GRAFT_REPO_ROOT/gpurun_out/bench_prof.log 2>&1
-rc=$?
-echo "rc=$rc"
-tail -3 $GRAFT_REPO_ROOT/gpurun_out/pytest_gpu.log
-exit $rc
+timeout -k 10 600 python3 bench.py > gpurun_out/bench.log 2>&1
+echo rc=$?
