@@ -12,14 +12,13 @@
 //     copies) — the reader applies s*c exactly as the reference's materialised copy would;
 //   * simplify() orders (hash, term-index) keys and sums each equal-hash group in term order:
 //       - N <= 64 terms: wave 0 alone. Each lane loads its term (hash + coefficients, one memory
-//         round trip), a bitonic network over __shfl_xor sorts the keys in registers, the
-//         coefficients follow by ds_bpermute, groups are summed by shuffles and compacted with
-//         ballot/popcount — no LDS traffic and no workgroup barrier;
-//       - larger: the operands are first staged into LDS with coalesced loads; then the order is
-//         built either by RANK MERGE (operator+/-, stack, addOneDim and products with few runs:
-//         the term list is a union of sorted runs, each key's rank is the sum of its lower bounds
-//         in the other runs — no sort), or by a register bitonic sort (256 x E keys, stages with
-//         j < E in registers, j < 64E by wave shuffles, only 3 stages through LDS);
+//         round trip), a bitonic network over DPP / permlane moves (wave.h) sorts the keys in
+//         registers, the coefficients follow by ds_bpermute, groups are summed by lane shifts and
+//         compacted with ballot/popcount — no workgroup barrier;
+//       - larger: the operands are first staged into LDS; the order is built by RANK MERGE: the
+//         term list is a union of sorted runs (the sources of a sum or stack; T1, T2 and the rows
+//         or columns of T3 for a product), and each key's rank is the sum of its lower bounds in
+//         the runs — no sort. The group sums park their kept values in HBM for the compaction;
 //   * every PZ carries TWO independent parts (nominal / interval inertial parameters). The
 //     reference runs RNEA twice (armour_main.cu:129,132) with identical centres and monomials —
 //     only `independent` differs — so one pass with dual independent parts replaces both;
@@ -92,7 +91,7 @@ struct Ctx {
     int* err;          // error word (LDS)
     double thr;
     unsigned long long* phase;  // optional large-operator phase cycle counters [8] (profiling)
-    int mode;          // diagnostics: bit 0 = no wave-0 path, bit 1 = no register sort (rank merge)
+    int mode;          // diagnostics: bit 0 = no wave-0 path
 };
 
 enum : int { ERR_ARENA = 1, ERR_SORTCAP = 2, ERR_LINKGEN = 4, ERR_OUTCAP = 8, ERR_HANDLES = 16 };
@@ -223,25 +222,6 @@ AI int block_scan(const Ctx& x, int* kp, int N) {
 }
 
 AI bool key_less(uint64_t h1, uint32_t i1, uint64_t h2, uint32_t i2) { return h1 < h2 || (h1 == h2 && i1 < i2); }
-
-// bitonic sort of P (power of two) keys in memory, whole group (host emulation and the global
-// fallback for operators beyond the LDS key capacity)
-AI void bitonic_mem(const Ctx& x, uint64_t* kh, uint32_t* ki, int P) {
-    const Grp& g = x.g;
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = g.tid; q < P / 2; q += g.n) {
-                const int i = 2 * j * (q / j) + (q % j);
-                const int l = i + j;
-                const bool asc = (i & k) == 0;
-                const uint64_t hi_ = kh[i], hl = kh[l];
-                const uint32_t ii = ki[i], il = ki[l];
-                const bool gt = key_less(hl, il, hi_, ii);
-                if (gt == asc) { kh[i] = hl; kh[l] = hi_; ki[i] = il; ki[l] = ii; }
-            }
-            g.sync();
-        }
-}
 
 // ---------------------------------------------------------------------------------------------
 // operands as the term generator sees them: a run of `cnt` monomials with hashes h[k] and
@@ -748,65 +728,6 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     SPHASE(12)
 }
 
-// ---- register bitonic: 256 x E keys, E per thread (element index tid * E + r) -----------------
-// xh/xi: exchange buffers for the cross-wave stages (>= P entries), oh/oi: the ordered output
-template <int E>
-__device__ inline __attribute__((always_inline)) void reg_bitonic(Ctx& x, const Terms& T, int N, uint64_t* xh, uint32_t* xi,
-                                                                  uint64_t* oh, uint32_t* oi) {
-    const int tid = x.g.tid;
-    uint64_t h[E];
-    uint32_t id[E];
-    UNR for (int r = 0; r < E; r++) {
-        const int idx = tid * E + r;
-        h[r] = idx < N ? T.hash(idx) : ~(uint64_t)0;
-        id[r] = (uint32_t)idx;
-    }
-    const int P = x.g.n * E;
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j < E) {
-                UNR for (int r = 0; r < E; r++) {
-                    if ((r & j) == 0) {
-                        const int r2 = r | j;
-                        const bool asc = ((tid * E + r) & k) == 0;
-                        const bool sw = asc ? key_less(h[r2], id[r2], h[r], id[r]) : key_less(h[r], id[r], h[r2], id[r2]);
-                        if (sw) {
-                            const uint64_t th = h[r]; h[r] = h[r2]; h[r2] = th;
-                            const uint32_t ti = id[r]; id[r] = id[r2]; id[r2] = ti;
-                        }
-                    }
-                }
-            } else if (j < 64 * E) {
-                const int m = j / E;
-                UNR for (int r = 0; r < E; r++) {
-                    // ds_bpermute here: with E keys per lane the exchange is throughput-bound and
-                    // the DPP form (two moves + select per dword) measured slower
-                    const uint64_t oh = __shfl_xor(h[r], m, 64);
-                    const uint32_t oi = __shfl_xor(id[r], m, 64);
-                    const int idx = tid * E + r;
-                    const bool asc = (idx & k) == 0, lower = (idx & j) == 0;
-                    const bool other_less = key_less(oh, oi, h[r], id[r]);
-                    if ((lower == asc) ? other_less : !other_less) { h[r] = oh; id[r] = oi; }
-                }
-            } else {
-                UNR for (int r = 0; r < E; r++) { xh[tid * E + r] = h[r]; xi[tid * E + r] = id[r]; }
-                x.g.sync();
-                UNR for (int r = 0; r < E; r++) {
-                    const int idx = tid * E + r;
-                    const uint64_t ph = xh[idx ^ j];
-                    const uint32_t pi = xi[idx ^ j];
-                    const bool asc = (idx & k) == 0, lower = (idx & j) == 0;
-                    const bool other_less = key_less(ph, pi, h[r], id[r]);
-                    if ((lower == asc) ? other_less : !other_less) { h[r] = ph; id[r] = pi; }
-                }
-                x.g.sync();
-            }
-        }
-    UNR for (int r = 0; r < E; r++) {
-        const int idx = tid * E + r;
-        if (idx < N) { oh[idx] = h[r]; oi[idx] = id[r]; }
-    }
-}
 #endif
 
 
@@ -825,49 +746,19 @@ AI bool order_keys(Ctx& x, const Terms& T, int N, KeyBufs& K) {
     const bool in_lds = N <= x.cap_lds;
     if (!in_lds) {
         K.kh = x.gkh; K.ki = x.gki; K.kp = x.gkp;
-        int P = 1;
-        while (P < N) P <<= 1;
-        if (P > x.cap_glb) return false;
+        if (N > x.cap_glb) return false;
     }
     uint64_t* kh = K.kh;
     uint32_t* ki = K.ki;
-    // order the keys: rank merge of sorted runs, or a sort
-    bool rank_ok = T.runs() <= 6 || (x.mode & 2);
-#if !defined(__HIP_DEVICE_COMPILE__)
-    rank_ok = true;
-#endif
-    if (rank_ok) {
-        for (int p = g.tid; p < N; p += g.n) {
-            const uint64_t h = T.hash(p);
-            const int r = T.rank(p, h);
-            kh[r] = h;
-            ki[r] = (uint32_t)p;
-        }
-    }
-#if defined(__HIP_DEVICE_COMPILE__)
-    else if (N <= 16 * g.n) {
-        // register bitonic over g.n * E keys; keys and exchanges in LDS up to its capacity, the
-        // rare larger operator exchanges and lands in the global buffers
-        const int E = N <= g.n ? 1 : N <= 2 * g.n ? 2 : N <= 4 * g.n ? 4 : N <= 8 * g.n ? 8 : 16;
-        uint64_t* xh = E * g.n <= x.cap_lds ? x.kh : x.gkh;
-        uint32_t* xi = E * g.n <= x.cap_lds ? x.ki : x.gki;
-        if (E == 1) reg_bitonic<1>(x, T, N, xh, xi, kh, ki);
-        else if (E == 2) reg_bitonic<2>(x, T, N, xh, xi, kh, ki);
-        else if (E == 4) reg_bitonic<4>(x, T, N, xh, xi, kh, ki);
-        else if (E == 8) reg_bitonic<8>(x, T, N, xh, xi, kh, ki);
-        else reg_bitonic<16>(x, T, N, xh, xi, kh, ki);
-    }
-#endif
-    else {
-        // many runs and beyond the register sort: bitonic in global memory
-        int P = 1;
-        while (P < N) P <<= 1;
-        for (int q = g.tid; q < P; q += g.n) {
-            kh[q] = q < N ? T.hash(q) : ~(uint64_t)0;
-            ki[q] = (uint32_t)q;
-        }
-        g.sync();
-        bitonic_mem(x, kh, ki, P);
+    // order the keys by rank merge of the sorted runs: a key's place is the sum of its lower
+    // bounds in the runs (Terms::rank). Measured against a register bitonic (the earlier path for
+    // more than 6 runs) it is faster at every run count the program produces, and it needs no
+    // padding, exchange buffers or sort registers.
+    for (int p = g.tid; p < N; p += g.n) {
+        const uint64_t h = T.hash(p);
+        const int r = T.rank(p, h);
+        kh[r] = h;
+        ki[r] = (uint32_t)p;
     }
     g.sync();
     return true;
