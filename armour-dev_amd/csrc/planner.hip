@@ -169,13 +169,12 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     }
     ra.arena_cap = 1 << 17;
     ra.gcap = 1 << 15;
-    ra.gout_cap = 3 << 13;  // kept values of operators up to 8192 terms (3x1) / 2730 (3x3)
     if ((rc = p->alloc(&p->d_jrs, jobs * NF))) return rc;
     if ((rc = p->alloc(&ra.arena_h, (size_t)p->reach_grid * ra.arena_cap)) ||
         (rc = p->alloc(&ra.arena_c, (size_t)p->reach_grid * ra.arena_cap * 3)) ||
         (rc = p->alloc(&ra.gkh, (size_t)p->reach_grid * ra.gcap)) || (rc = p->alloc(&ra.gki, (size_t)p->reach_grid * ra.gcap)) ||
         (rc = p->alloc(&ra.gkp, (size_t)p->reach_grid * ra.gcap)) ||
-        (rc = p->alloc(&ra.gout, (size_t)p->reach_grid * ra.gout_cap)))
+        (rc = p->alloc(&ra.gout, (size_t)p->reach_grid * ra.gcap * 9)))
         return rc;
     // NLP
     NlpDev& d = p->d;

@@ -82,8 +82,7 @@ struct Ctx {
     uint32_t* gki;
     int* gkp;
     int cap_glb;
-    double* gout;      // kept group values of the simplify in flight, by key position (HBM)
-    int gout_cap;      // doubles
+    double* gout;      // group sums of the simplify in flight, by key position (HBM): cap_glb * 9
     double* stage;     // operand staging (LDS), stage_cap doubles
     int stage_cap;
     double* red;       // reduction scratch (LDS): [waves * 18] on device, [n * 18] in the emulation
@@ -786,12 +785,10 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
     const uint64_t* kh = K.kh;
     const uint32_t* ki = K.ki;
     int* kp = K.kp;
-    double red[Pol::NR], acc[NV], tmp[NV], out[n];
-    UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
-    UNR for (int e = 0; e < n; e++) out[e] = 0.0;
-    // the kept groups' values wait in gout for the compaction pass (same thread, same q), which
-    // then copies instead of summing the group again; without room it recomputes them
-    const bool cache = x.gout && (long)N * n <= x.gout_cap;
+    // pass 1: each group head sums its group in term order and parks the NV sums in gout (HBM,
+    // by key position); only the keep flag goes on. No reduction slots are live here — the sum
+    // loop is the register-heavy part (a 3x3 block product per term).
+    double acc[NV], tmp[NV];
     for (int q = g.tid; q < N; q += g.n) {
         const bool head = q == 0 || kh[q] != kh[q - 1];
         int keep = 0;
@@ -801,8 +798,10 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
                 pol.term(T, ki[r], tmp);
                 UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + tmp[e];
             }
-            keep = pol.group(acc, out, red) ? 1 : 0;
-            if (keep && cache) UNR for (int e = 0; e < n; e++) x.gout[(long)q * n + e] = out[e];
+            double o1[n], r1[Pol::NR];  // dead: the decision only
+            UNR for (int e = 0; e < Pol::NR; e++) r1[e] = 0.0;
+            keep = pol.group(acc, o1, r1) ? 1 : 0;
+            UNR for (int e = 0; e < NV; e++) x.gout[(long)q * NV + e] = acc[e];
         }
         kp[q] = keep;
     }
@@ -815,25 +814,20 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
     }
     g.sync();
     PHASE(3)
+    // pass 2, same thread and q order as pass 1: the group decision again from the parked sums,
+    // its pruned / kept amounts into the reduction slots (the order pass 1 would have used), and
+    // the kept rows written at their compacted position
     const long hoff = x.H[o].hoff, coff = x.H[o].coff;
-    if (x.H[o].cnt == K_) {
-        double dummy[Pol::NR];
-        for (int q = g.tid; q < N; q += g.n) {
-            const bool head = q == 0 || kh[q] != kh[q - 1];
-            if (!head) continue;
-            const bool keep = (q + 1 < N) ? (kp[q + 1] != kp[q]) : (kp[q] != K_);
-            if (!keep) continue;
-            if (cache) {
-                UNR for (int e = 0; e < n; e++) out[e] = x.gout[(long)q * n + e];
-            } else {
-                pol.term(T, ki[q], acc);
-                for (int r = q + 1; r < N && kh[r] == kh[q]; r++) {
-                    pol.term(T, ki[r], tmp);
-                    UNR for (int e = 0; e < NV; e++) acc[e] = acc[e] + tmp[e];
-                }
-                UNR for (int e = 0; e < Pol::NR; e++) dummy[e] = 0.0;
-                pol.group(acc, out, dummy);
-            }
+    const bool ok = x.H[o].cnt == K_;
+    double red[Pol::NR], out[n];
+    UNR for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
+    for (int q = g.tid; q < N; q += g.n) {
+        const bool head = q == 0 || kh[q] != kh[q - 1];
+        if (!head) continue;
+        UNR for (int e = 0; e < NV; e++) acc[e] = x.gout[(long)q * NV + e];
+        UNR for (int e = 0; e < n; e++) out[e] = 0.0;
+        const bool keep = pol.group(acc, out, red);
+        if (keep && ok) {
             const long pos = kp[q];
             x.A->h[hoff + pos] = kh[q];
             double* dst = x.A->c + coff + pos * n;

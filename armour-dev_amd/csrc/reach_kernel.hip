@@ -52,8 +52,7 @@ struct ReachArgs {
     uint32_t* gki;
     int* gkp;
     int gcap;
-    double* gout;        // [grid][gout_cap]
-    int gout_cap;
+    double* gout;        // [grid][gcap * 9]
     unsigned long long* bytes;  // algorithmic monomial bytes of all jobs (one atomic per job)
     unsigned long long* prof;   // optional per-op [cycles, terms] (null: off)
     int mode;                   // engine diagnostics (Ctx::mode)
@@ -90,8 +89,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREA
     x.gki = a.gki + (long)blockIdx.x * a.gcap;
     x.gkp = a.gkp + (long)blockIdx.x * a.gcap;
     x.cap_glb = a.gcap;
-    x.gout = a.gout + (long)blockIdx.x * a.gout_cap;
-    x.gout_cap = a.gout_cap;
+    x.gout = a.gout + (long)blockIdx.x * a.gcap * 9;
     x.stage = stage;
     x.stage_cap = STAGE_DOUBLES;
     x.red = red;

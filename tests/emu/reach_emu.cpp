@@ -52,7 +52,7 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     x.kh = kh.data(); x.ki = ki.data(); x.kp = kp.data(); x.cap_lds = kcap;
     x.gkh = kh.data(); x.gki = ki.data(); x.gkp = kp.data(); x.cap_glb = kcap;
     std::vector<double> gout(9 * (size_t)kcap);
-    x.gout = gout.data(); x.gout_cap = 9 * kcap;
+    x.gout = gout.data();
     std::vector<double> stage(4096);
     x.stage = stage.data();
     x.stage_cap = 4096;
