@@ -268,7 +268,7 @@ AI int lower_bound(const uint64_t* h, int cnt, uint64_t key) {
     }
     return lo;
 }
-// same over the T3 row i of a product: keys ha + hb[j]
+// same over the T3 row i of a product: keys off + h[j]
 AI int lower_bound_off(const uint64_t* h, int cnt, uint64_t off, uint64_t key) {
     int lo = 0, len = cnt;
     while (len > 0) {
@@ -376,40 +376,29 @@ struct Terms {
     }
     // rank of term p (hash h) in the (hash, term index) order of the whole list
     AI int rank(int p, uint64_t h) const {
-        int r = 0;
+        // A run's equal key (at most one per run) precedes term p when its term index is lower,
+        // which is decided by the run alone: earlier sources / T1 / T2 / earlier T3 rows precede,
+        // later ones follow. So a preceding run counts keys <= h (a search for h + 1), a following
+        // one keys < h, and the own run contributes the own index — no tie probe.
+        const uint64_t h1 = h + 1;  // hashes stay below 2^63
         if (kind == 1) {
             int s, k;
             which(p, s, k);
-            UNR for (int t = 0; t < 3; t++) {
-                if (t >= ns) continue;
-                if (t == s) { r += k; continue; }
-                int lb = lower_bound(S[t].h, S[t].cnt, h);
-                if (t < s && lb < S[t].cnt && S[t].h[lb] == h) lb++;
-                r += lb;
-            }
+            int r = k;
+            UNR for (int t = 0; t < 3; t++)
+                if (t < ns && t != s) r += lower_bound(S[t].h, S[t].cnt, t < s ? h1 : h);
             return r;
         }
         const int na = S[0].cnt, nb = S[1].cnt;
-        // T1: indices 0..na-1
-        {
-            int lb = lower_bound(S[0].h, na, h);
-            if (lb < na && S[0].h[lb] == h && lb < p) lb++;
-            r += lb;
-        }
-        // T2: indices na..na+nb-1
-        {
-            int lb = lower_bound(S[1].h, nb, h);
-            if (lb < nb && S[1].h[lb] == h && na + lb < p) lb++;
-            r += lb;
-        }
         const int base = na + nb;
+        const int seg = p < na ? 0 : (p < base ? 1 : 2);
+        int r = seg == 0 ? p : lower_bound(S[0].h, na, h1);             // T1
+        r += seg == 1 ? p - na : lower_bound(S[1].h, nb, seg == 2 ? h1 : h);  // T2
         if (na <= nb) {
-            for (int i = 0; i < na; i++) {
-                const uint64_t hai = S[0].h[i];
-                int lb = lower_bound_off(S[1].h, nb, hai, h);
-                if (lb < nb && hai + S[1].h[lb] == h && base + i * nb + lb < p) lb++;
-                r += lb;
-            }
+            int i0 = -1, j0 = 0;
+            if (seg == 2) split(p - base, i0, j0);
+            for (int i = 0; i < na; i++)
+                r += i == i0 ? j0 : lower_bound_off(S[1].h, nb, S[0].h[i], i < i0 ? h1 : h);
         } else {
             for (int j = 0; j < nb; j++) {
                 const uint64_t hbj = S[1].h[j];
