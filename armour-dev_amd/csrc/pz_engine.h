@@ -454,17 +454,39 @@ AI void stage_sources(Ctx& x, Terms& T) {
     }
 }
 
+// shared counters of the workgroup, updated by one lane per op — or by several lanes at once in
+// a lane-parallel group of thread-0 ops (reach.h), hence LDS atomics on the device
+AI void err_or(const Ctx& x, int bits) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicOr(x.err, bits);
+#else
+    *x.err |= bits;
+#endif
+}
+AI void bytes_add(const Ctx& x, double b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicAdd(&x.A->bytes, b);
+#else
+    x.A->bytes += b;
+#endif
+}
 AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
     h.stride = stride;
-    if (x.A->hused + K > x.A->hcap || x.A->cused + (long)K * stride > x.A->ccap) {
-        *x.err |= ERR_ARENA;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const long h0 = (long)atomicAdd((unsigned long long*)&x.A->hused, (unsigned long long)K);
+    const long c0 = (long)atomicAdd((unsigned long long*)&x.A->cused, (unsigned long long)K * stride);
+#else
+    const long h0 = x.A->hused, c0 = x.A->cused;
+    x.A->hused += K;
+    x.A->cused += (long)K * stride;
+#endif
+    if (h0 + K > x.A->hcap || c0 + (long)K * stride > x.A->ccap) {
+        err_or(x, ERR_ARENA);
         h.cnt = 0; h.hoff = 0; h.coff = 0;
     } else {
-        h.hoff = x.A->hused;
-        h.coff = x.A->cused;
+        h.hoff = h0;
+        h.coff = c0;
         h.cnt = K;
-        x.A->hused += K;
-        x.A->cused += (long)K * stride;
     }
 }
 

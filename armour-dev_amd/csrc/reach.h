@@ -186,11 +186,11 @@ struct Op {
     int o, a, b, c;
     int i;
     int sync;   // barrier after this op
-    int pad;
+    int par;    // > 1: first of a lane-parallel group of par independent thread-0 ops of one code
     double s;
 };
 
-constexpr int MAX_SLOTS = 68;
+constexpr int MAX_SLOTS = 76;
 
 // thread-0 bodies are inlined too: an out-of-line variant (stack arrays passed through a lambda
 // into a nested out-of-line call) was miscompiled for gfx950 — tools/dump_ops.py localised it to
@@ -265,7 +265,7 @@ T0FN void t0_view(Ctx& x, int o, int a, int e, int scaled, double s) {
     h.comp = e >= 0 ? e : P.comp;
     h.scaled = scaled;
     h.scale = scaled ? s : 1.0;
-    if (P.comp >= 0 || P.scaled) *x.err |= ERR_HANDLES;  // views of views never occur in this program
+    if (P.comp >= 0 || P.scaled) err_or(x, ERR_HANDLES);  // views of views never occur in this program
     for (int q = 0; q < n; q++) {
         const int src = e >= 0 ? e : q;
         double c = cen(x, P)[src], i0 = ind(x, P, 0)[src], i1 = ind(x, P, 1)[src], ab = abs_(x, P)[src];
@@ -297,7 +297,7 @@ T0FN void t0_transpose(Ctx& x, int o, int a) {
             for (int i = 0; i < A.R; i++)
                 for (int jj = 0; jj < A.C; jj++) x.A->c[h.coff + (long)k * n + jj + i * A.C] = m[i + jj * A.R];
         }
-    x.A->bytes += 2.0 * A.cnt * (8.0 + 8.0 * n);
+    bytes_add(x, 2.0 * A.cnt * (8.0 + 8.0 * n));
 }
 
 T0FN void t0_make_1d(Ctx& x, int o, const JrsJoint& J, int i, int v) {
@@ -362,12 +362,12 @@ T0FN void t0_emit_link(Ctx& x, const ReachOut& out, long j, int a, int l) {
                 out.link_hash[base * CAP_LM + kk] = (uint16_t)hh;
                 for (int e = 0; e < 3; e++) out.link_coef[(base * CAP_LM + kk) * 3 + e] = c[e];
             } else {
-                *x.err |= ERR_OUTCAP;
+                err_or(x, ERR_OUTCAP);
             }
             kk++;
         } else if (hh < HASH_K_LINKS_ONLY && (hh & K_MASK) == 0) {
             if (jg < 3) { for (int e = 0; e < 3; e++) gl[e + 3 * jg] = c[e]; }
-            else *x.err |= ERR_LINKGEN;
+            else err_or(x, ERR_LINKGEN);
             jg++;
         } else {
             for (int e = 0; e < 3; e++) rad[e] += fabs(c[e]);
@@ -399,7 +399,7 @@ T0FN void t0_emit_torque(Ctx& x, const ReachOut& out, long j, int a, int i, doub
                 out.tq_hash[base * CAP_UM + kk] = (uint16_t)hh;
                 out.tq_coef[base * CAP_UM + kk] = c;
             } else {
-                *x.err |= ERR_OUTCAP;
+                err_or(x, ERR_OUTCAP);
             }
             kk++;
         } else {
@@ -488,6 +488,7 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 #endif
     for (int pc = 0; pc < nops; pc++) {
         const Op op = prog[pc];
+        const int par = op.par > 1 ? op.par : 1;  // ops pc .. pc + par - 1 run as one group
 #if defined(__HIP_DEVICE_COMPILE__)
         long long c0 = 0;
         if (stamp) {
@@ -505,27 +506,39 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                 for (int i = tid; i < NF; i += x.g.n) jrs[i] = jrs_in ? jrs_in[i] : jrs_joint(rp, T, t, i, q0[i], qd0[i], qdd0[i]);
 #endif
                 break;
-            case OP_MAKE1D: if (tid == 0) t0_make_1d(x, op.o, jrs[op.i], op.i, op.b); break;
-            case OP_MAKEROT: if (tid == 0) t0_make_rot(x, op.o, rp, jrs[op.i], op.i); break;
-            case OP_MAKEBOX: if (tid == 0) t0_make_box(x, op.o, rp, op.i); break;
+            case OP_MAKE1D:
+            case OP_MAKEROT:
+            case OP_MAKEBOX:
             case OP_CONST:
-                if (tid == 0) {
-                    if (op.a == CONST_RPY) t0_const(x, op.o, 3, 3, rp.rpy[op.i], 0.0);
-                    else if (op.a == CONST_TRANS) t0_const(x, op.o, 3, 1, &rp.trans[3 * op.i], 0.0);
-                    else if (op.a == CONST_MASS) t0_const(x, op.o, 1, 1, &rp.mass[op.i], rp.mass_uncertainty);
-                    else t0_const(x, op.o, 3, 3, &rp.inertia[9 * op.i], rp.inertia_uncertainty);
-                }
-                break;
             case OP_ZERO:
-                if (tid == 0) {
-                    hdr_init(x, x.H[op.o], op.b, op.c);
-                    if (op.i) cen(x, x.H[op.o])[2] = rp.gravity;
+            case OP_VIEW:
+            case OP_TRANSPOSE:
+            case OP_EMIT_LINK:
+            case OP_EMIT_TORQUE:
+                // thread-0 ops; a group of par independent ones runs one per lane of wave 0
+                for (int mi = tid; mi < par; mi += x.g.n) {
+                    const Op m = mi == 0 ? op : prog[pc + mi];
+                    switch (m.code) {
+                        case OP_MAKE1D: t0_make_1d(x, m.o, jrs[m.i], m.i, m.b); break;
+                        case OP_MAKEROT: t0_make_rot(x, m.o, rp, jrs[m.i], m.i); break;
+                        case OP_MAKEBOX: t0_make_box(x, m.o, rp, m.i); break;
+                        case OP_CONST:
+                            if (m.a == CONST_RPY) t0_const(x, m.o, 3, 3, rp.rpy[m.i], 0.0);
+                            else if (m.a == CONST_TRANS) t0_const(x, m.o, 3, 1, &rp.trans[3 * m.i], 0.0);
+                            else if (m.a == CONST_MASS) t0_const(x, m.o, 1, 1, &rp.mass[m.i], rp.mass_uncertainty);
+                            else t0_const(x, m.o, 3, 3, &rp.inertia[9 * m.i], rp.inertia_uncertainty);
+                            break;
+                        case OP_ZERO:
+                            hdr_init(x, x.H[m.o], m.b, m.c);
+                            if (m.i) cen(x, x.H[m.o])[2] = rp.gravity;
+                            break;
+                        case OP_VIEW: t0_view(x, m.o, m.a, m.i, m.b, m.s); break;
+                        case OP_TRANSPOSE: t0_transpose(x, m.o, m.a); break;
+                        case OP_EMIT_LINK: t0_emit_link(x, out, j, m.a, m.i); break;
+                        default: t0_emit_torque(x, out, j, m.a, m.i, rdist, ured); break;
+                    }
                 }
                 break;
-            case OP_VIEW: if (tid == 0) t0_view(x, op.o, op.a, op.i, op.b, op.s); break;
-            case OP_TRANSPOSE: if (tid == 0) t0_transpose(x, op.o, op.a); break;
-            case OP_EMIT_LINK: if (tid == 0) t0_emit_link(x, out, j, op.a, op.i); break;
-            case OP_EMIT_TORQUE: if (tid == 0) t0_emit_torque(x, out, j, op.a, op.i, rdist, ured); break;
             case OP_TORQUE_RADIUS: if (tid == 0) t0_torque_radius(rp, out, j, rdist, ured); break;
             case OP_CROSS_C: {
                 const double* v = op.b == VEC_TRANS ? &rp.trans[3 * op.c] : &rp.com[3 * op.c];
@@ -614,14 +627,17 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 #if !defined(__HIP_DEVICE_COMPILE__)
         if (g_op_stats && op.o >= 0) g_op_stats[8 * pc + 7] = x.H[op.o].cnt;
 #endif
-        if (dump && op.o >= 0) {
+        if (dump) {
             x.g.sync();
-            if (tid == 0) {
-                const PZH& h = x.H[op.o];
-                double* d = dump + (long)pc * DUMP_W;
-                d[0] = h.cnt; d[1] = h.R * h.C; d[2] = cen(x, h)[0]; d[3] = cen(x, h)[1]; d[4] = cen(x, h)[2];
-                d[5] = ind(x, h, 0)[0]; d[6] = ind(x, h, 1)[0]; d[7] = abs_(x, h)[0];
-            }
+            if (tid == 0)
+                for (int mi = 0; mi < par; mi++) {
+                    const int mo = prog[pc + mi].o;
+                    if (mo < 0) continue;
+                    const PZH& h = x.H[mo];
+                    double* d = dump + (long)(pc + mi) * DUMP_W;
+                    d[0] = h.cnt; d[1] = h.R * h.C; d[2] = cen(x, h)[0]; d[3] = cen(x, h)[1]; d[4] = cen(x, h)[2];
+                    d[5] = ind(x, h, 0)[0]; d[6] = ind(x, h, 1)[0]; d[7] = abs_(x, h)[0];
+                }
             x.g.sync();
         }
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -635,6 +651,7 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
             }
         }
 #endif
+        pc += par - 1;
     }
 }
 
@@ -680,7 +697,7 @@ struct ProgramBuilder {
     void rel(std::initializer_list<int> l) { for (int s : l) rel(s); }
     void emit(int code, int o = -1, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
         Op op;
-        op.code = code; op.o = o; op.a = a; op.b = b; op.c = c; op.i = i; op.s = s; op.sync = 1; op.pad = 0;
+        op.code = code; op.o = o; op.a = a; op.b = b; op.c = c; op.i = i; op.s = s; op.sync = 1; op.par = 0;
         ops.push_back(op);
     }
     int out(int code, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
@@ -761,10 +778,14 @@ struct ProgramBuilder {
         const int NJ = rp.num_joints;
         int R[MAX_J + 1], RT[MAX_J], QD[NF], QDA[NF], QDD[NF];
         emit(OP_JRS);
+        // ops of one kind that do not depend on each other are emitted back to back, so that
+        // group() can run them lane-parallel
         for (int i = 0; i < NF; i++) {
             QD[i] = out(OP_MAKE1D, 0, 0, 0, i);
             QDA[i] = out(OP_MAKE1D, 0, 1, 0, i);
             QDD[i] = out(OP_MAKE1D, 0, 2, 0, i);
+        }
+        for (int i = 0; i < NF; i++) {
             if (rp.axes[i] != 0) {
                 const int rot = out(OP_MAKEROT, 0, 0, 0, i);
                 const int c = cnst(CONST_RPY, i);
@@ -773,17 +794,14 @@ struct ProgramBuilder {
             } else {
                 R[i] = cnst(CONST_RPY, i);
             }
-            RT[i] = out(OP_TRANSPOSE, R[i]);
         }
-        for (int i = NF; i < NJ; i++) {
-            R[i] = cnst(CONST_RPY, i);
-            RT[i] = out(OP_TRANSPOSE, R[i]);
-        }
+        for (int i = NF; i < NJ; i++) R[i] = cnst(CONST_RPY, i);
+        for (int i = 0; i < NJ; i++) RT[i] = out(OP_TRANSPOSE, R[i]);
         R[NJ] = cnst(CONST_RPY, MAX_J);  // PZsparse(0, 0, 0)
 
         // forward kinematics (Dynamics.cu:69-81) + reduce_link_PZ (armour_main.cu:124-126)
         {
-            int FKR = cnst(CONST_RPY, MAX_J), FKT = zero(3, 1);
+            int FKR = cnst(CONST_RPY, MAX_J), FKT = zero(3, 1), links[MAX_J];
             for (int i = 0; i < NJ; i++) {
                 const int P = cnst(CONST_TRANS, i);
                 const int tmp = mul(FKR, P);
@@ -795,11 +813,12 @@ struct ProgramBuilder {
                 FKR = fkr;
                 const int box = out(OP_MAKEBOX, 0, 0, 0, i);
                 const int tmp2 = mul(FKR, box);
-                const int link = add(tmp2, FKT);
-                emit(OP_EMIT_LINK, -1, link, 0, 0, i);
-                rel({box, tmp2, link});
+                links[i] = add(tmp2, FKT);
+                rel({box, tmp2});
             }
             rel({FKR, FKT});
+            for (int i = 0; i < NJ; i++) emit(OP_EMIT_LINK, -1, links[i], 0, 0, i);
+            for (int i = 0; i < NJ; i++) rel(links[i]);
         }
 
         // RNEA, nominal and interval fused (Dynamics.cu:83-181)
@@ -874,7 +893,8 @@ struct ProgramBuilder {
             }
         }
         rel({W, WDOT, WAUX, LIN});
-        int FF = zero(3, 1), NN = zero(3, 1);
+        int FF = zero(3, 1), NN = zero(3, 1), us[MAX_J];
+        for (int i = 0; i < MAX_J; i++) us[i] = -1;
         for (int i = NJ - 1; i >= 0; i--) {
             // line 29: n = N + R*n + cross(com, F) + cross(p_{i+1}, R*f); R*f evaluated once
             const int t1 = mul(R[i + 1], NN);
@@ -896,11 +916,14 @@ struct ProgramBuilder {
                 const int s1 = scaled(QDD[i], rp.armature[i]);
                 const int u1 = add(e, s1);
                 const int s2 = scaled(QD[i], rp.damping[i]);
-                const int u = add(u1, s2);
-                emit(OP_EMIT_TORQUE, -1, u, 0, 0, i);
-                rel({e, s1, u1, s2, u});
+                us[i] = add(u1, s2);
+                rel({e, s1, u1, s2});
             }
         }
+        for (int i = NJ - 1; i >= 0; i--)
+            if (us[i] >= 0) emit(OP_EMIT_TORQUE, -1, us[i], 0, 0, i);
+        for (int i = NJ - 1; i >= 0; i--)
+            if (us[i] >= 0) rel(us[i]);
         emit(OP_TORQUE_RADIUS);
         // thread-0 ops chained back to back need no barrier between them
         auto t0_only = [](int c) {
@@ -909,6 +932,33 @@ struct ProgramBuilder {
         };
         for (size_t k = 0; k + 1 < ops.size(); k++)
             if (t0_only(ops[k].code) && t0_only(ops[k + 1].code)) ops[k].sync = 0;
+        group(t0_only);
+    }
+    // consecutive thread-0 ops of one code none of which reads another's output become one
+    // lane-parallel group (at most a wave); a barrier follows every group
+    template <class F>
+    void group(F t0_only) {
+        auto reads = [](const Op& op, int slot) {
+            return (op.code == OP_VIEW || op.code == OP_TRANSPOSE || op.code == OP_EMIT_LINK || op.code == OP_EMIT_TORQUE) &&
+                   op.a == slot;
+        };
+        for (size_t k = 0; k < ops.size();) {
+            size_t e = k + 1;
+            if (t0_only(ops[k].code)) {
+                while (e < ops.size() && e - k < 64 && ops[e].code == ops[k].code) {
+                    bool dep = false;
+                    for (size_t q = k; q < e; q++) dep = dep || (ops[q].o >= 0 && reads(ops[e], ops[q].o));
+                    if (dep) break;
+                    e++;
+                }
+            }
+            if (e - k > 1) {
+                ops[k].par = (int)(e - k);
+                ops[k].sync = 1;
+                if (k > 0) ops[k - 1].sync = 1;  // members on other lanes read what thread 0 wrote
+            }
+            k = e;
+        }
     }
 };
 
