@@ -201,44 +201,54 @@ constexpr int MAX_SLOTS = 76;
 
 // PZ from raw candidate monomials with the reference constructor's simplify (PZsparse.cu:120-205)
 T0FN void t0_make_raw(Ctx& x, int o, int R, int C, const double* center, int nc, const uint64_t* hs, const double (*cf)[9]) {
+    // the reference's stable sort + merge + prune of <= 4 monomials, written with static indices
+    // only (a run-time index into these small arrays would put them in scratch memory): members
+    // of an equal-hash group are summed in index order (the stable order), pruned amounts and
+    // |kept| sums are added in hash order, kept rows land at their hash rank
+    constexpr int M = 4;
     const int n = R * C;
-    int ord[4];
-    for (int i = 0; i < nc; i++) ord[i] = i;
-    for (int i = 1; i < nc; i++)  // insertion sort by hash (stable)
-        for (int j = i; j > 0 && hs[ord[j]] < hs[ord[j - 1]]; j--) { const int t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
-    double keep_c[4][9];
-    uint64_t keep_h[4];
-    int K = 0;
-    double red[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    int i = 0;
-    while (i < nc) {
-        double acc[9];
-        for (int e = 0; e < 9; e++) acc[e] = e < n ? cf[ord[i]][e] : 0.0;
-        int j = i + 1;
-        for (; j < nc && hs[ord[j]] == hs[ord[i]]; j++)
-            for (int e = 0; e < n; e++) acc[e] = acc[e] + cf[ord[j]][e];
-        if (frob_norm(acc, n) <= x.thr) {
-            for (int e = 0; e < n; e++) red[e] = red[e] + fabs(acc[e]);
-        } else {
-            for (int e = 0; e < 9; e++) keep_c[K][e] = acc[e];
-            keep_h[K] = hs[ord[i]];
-            K++;
-        }
-        i = j;
+    uint64_t h[M];
+    UNR for (int m = 0; m < M; m++) h[m] = m < nc ? hs[m] : ~(uint64_t)0;
+    bool head[M], keep[M];
+    double acc[M][9];
+    UNR for (int m = 0; m < M; m++) {
+        head[m] = m < nc;
+        UNR for (int m2 = 0; m2 < m; m2++) if (h[m2] == h[m]) head[m] = false;
+        UNR for (int e = 0; e < 9; e++) acc[m][e] = (m < nc && e < n) ? cf[m][e] : 0.0;
+        UNR for (int m2 = m + 1; m2 < M; m2++)
+            if (m2 < nc && h[m2] == h[m]) UNR for (int e = 0; e < 9; e++) if (e < n) acc[m][e] = acc[m][e] + cf[m2][e];
+        keep[m] = head[m] && !(frob_norm(acc[m], n) <= x.thr);
     }
-    PZH& h = x.H[o];
-    hdr_init(x, h, R, C);
-    for (int e = 0; e < n; e++) cen(x, h)[e] = center[e];
-    if (frob_norm(red, n) != 0)
-        for (int e = 0; e < n; e++) { ind(x, h, 0)[e] += red[e]; ind(x, h, 1)[e] += red[e]; }
-    for (int k = 0; k < K; k++)
-        for (int e = 0; e < n; e++) abs_(x, h)[e] += fabs(keep_c[k][e]);
-    arena_alloc_t0(x, h, K, n);
-    if (h.cnt == K)
-        for (int k = 0; k < K; k++) {
-            x.A->h[h.hoff + k] = keep_h[k];
-            for (int e = 0; e < n; e++) x.A->c[h.coff + (long)k * n + e] = keep_c[k][e];
+    int rk[M], pos[M], K = 0;
+    UNR for (int m = 0; m < M; m++) {
+        rk[m] = 0;
+        pos[m] = 0;
+        UNR for (int m2 = 0; m2 < M; m2++) {
+            if (head[m2] && h[m2] < h[m]) rk[m]++;
+            if (keep[m2] && h[m2] < h[m]) pos[m]++;
         }
+        K += keep[m] ? 1 : 0;
+    }
+    double red[9], ab[9];
+    UNR for (int e = 0; e < 9; e++) { red[e] = 0.0; ab[e] = 0.0; }
+    UNR for (int r = 0; r < M; r++)
+        UNR for (int m = 0; m < M; m++) {
+            if (head[m] && !keep[m] && rk[m] == r) UNR for (int e = 0; e < 9; e++) red[e] = red[e] + fabs(acc[m][e]);
+            if (keep[m] && pos[m] == r) UNR for (int e = 0; e < 9; e++) ab[e] = ab[e] + fabs(acc[m][e]);
+        }
+    PZH& hd = x.H[o];
+    hdr_init(x, hd, R, C);
+    for (int e = 0; e < n; e++) cen(x, hd)[e] = center[e];
+    if (frob_norm(red, n) != 0)
+        for (int e = 0; e < n; e++) { ind(x, hd, 0)[e] += red[e]; ind(x, hd, 1)[e] += red[e]; }
+    UNR for (int e = 0; e < 9; e++) if (e < n) abs_(x, hd)[e] += ab[e];
+    arena_alloc_t0(x, hd, K, n);
+    if (hd.cnt == K)
+        UNR for (int m = 0; m < M; m++)
+            if (keep[m]) {
+                x.A->h[hd.hoff + pos[m]] = h[m];
+                UNR for (int e = 0; e < 9; e++) if (e < n) x.A->c[hd.coff + (long)pos[m] * n + e] = acc[m][e];
+            }
 }
 
 // constant PZ (no monomials): PZsparse(const MatrixXd&, double uncertainty) (PZsparse.cu:75-98);
