@@ -1,0 +1,111 @@
+// armour-mi355x — reach-set kernel, bundle form (lane_engine.h): one 512-thread workgroup per
+// bundle of 64 consecutive (world, interval) jobs, lane = job. Persistent grid over bundles; each
+// resident workgroup owns an HBM arena (union hashes, presence masks, [row][64] coefficients), a
+// header pool ([row][64]), global key buffers for operators beyond the LDS key capacity and the
+// group-value buffer between the two simplify passes. LDS (~90 KB) holds the handle table, keys,
+// group heads, staged operand hashes and the cross-wave reduction rows: one workgroup (8 waves,
+// two per SIMD) per CU.
+#include "lane_engine.h"
+
+namespace armour {
+namespace lane {
+
+struct LaneArgs {
+    int W, T;
+    const JrsJoint* jrs;   // [W][T][NF] from jrs_kernel
+    const Op* prog;
+    int nops;
+    const int* slot_off;   // payload rows of every handle slot in the pool
+    int nslots;
+    long pool_rows;        // per workgroup
+    double* pool;          // [grid][pool_rows][LG]
+    uint64_t* arena_h;     // [grid][hcap]
+    uint64_t* arena_m;     // [grid][hcap]
+    double* arena_c;       // [grid][ccap][LG]
+    long hcap, ccap;
+    uint64_t* gkh;         // [grid][gcap]
+    uint32_t* gki;
+    int* gkp;              // [grid][gcap + 1]
+    int* ggp;              // [grid][gcap + 1]
+    int gcap;
+    double* gout;          // [grid][ocap][9][LG]
+    uint64_t* gm;          // [grid][ocap]
+    int ocap;
+    unsigned long long* bytes;
+    double* dump;          // optional [nops][DUMP_W][LG] of bundle 0 (null: off)
+    unsigned long long* prof;  // optional [2 * nops + 16] per-op cycles/terms + phase cycles
+};
+
+__global__ __attribute__((amdgpu_flat_work_group_size(LT, LT))) void lane_reach_kernel(const RobotParams* __restrict__ rpp, LaneArgs a, ReachOut out) {
+    __shared__ LH H[MAX_SLOTS];
+    __shared__ uint64_t kh[LKEYS];
+    __shared__ uint32_t ki[LKEYS];
+    __shared__ int kp[LKEYS + 1];
+    __shared__ int gp[LKEYS + 1];
+    __shared__ uint64_t stage[LSTAGE];
+    __shared__ uint64_t rmask[128];
+    __shared__ double red[(LW - 1) * RCH * LG];
+    __shared__ double scr[2 * NF * LG];
+    __shared__ int iscan[LW];
+    __shared__ LArena arena;
+    __shared__ int err;
+
+    const RobotParams& rp = *rpp;
+    const long wg = blockIdx.x;
+    LCtx x;
+    x.tid = threadIdx.x;
+    x.wave = x.tid >> 6;
+    x.lane = x.tid & 63;
+    x.H = H;
+    x.pool = a.pool + wg * a.pool_rows * LG;
+    x.A = &arena;
+    x.kh = kh; x.ki = ki; x.kp = kp; x.gp = gp; x.cap_lds = LKEYS;
+    x.gkh = a.gkh + wg * a.gcap;
+    x.gki = a.gki + wg * a.gcap;
+    x.gkp = a.gkp + wg * (a.gcap + 1);
+    x.ggp = a.ggp + wg * (a.gcap + 1);
+    x.cap_glb = a.gcap;
+    x.gout = a.gout + wg * (long)a.ocap * 9 * LG;
+    x.gm = a.gm + wg * (long)a.ocap;
+    x.cap_out = a.ocap;
+    x.rmask = rmask;
+    x.stage = stage;
+    x.stage_cap = LSTAGE;
+    x.red = red;
+    x.scr = scr;
+    x.iscan = iscan;
+    x.err = &err;
+    x.thr = rp.simplify_threshold;
+    x.prof = a.prof;
+    x.nops = a.nops;
+
+    const long njobs = (long)a.W * a.T;
+    const long nb = (njobs + LG - 1) / LG;
+    for (long b = blockIdx.x; b < nb; b += gridDim.x) {
+        if (x.tid == 0) {
+            arena.h = a.arena_h + wg * a.hcap;
+            arena.m = a.arena_m + wg * a.hcap;
+            arena.c = a.arena_c + wg * a.ccap * LG;
+            arena.hcap = a.hcap;
+            arena.ccap = a.ccap;
+            arena.hused = 0;
+            arena.cused = 0;
+            arena.bytes = 0;
+            err = 0;
+        }
+        for (int k = x.tid; k < a.nslots; k += LT) H[k].off = a.slot_off[k];
+        const long job = b * LG + x.lane;
+        x.valid = job < njobs;
+        x.job = x.valid ? job : njobs - 1;
+        x.jrs = a.jrs + x.job * NF;
+        __syncthreads();
+        run_program(x, rp, a.prog, a.nops, out, b == 0 ? a.dump : nullptr);
+        __syncthreads();
+        if (err && x.wave == 0 && x.valid) atomicOr(&out.err[x.job / a.T], err);
+        if (x.tid == 0) atomicAdd(a.bytes, arena.bytes);
+        __syncthreads();
+    }
+}
+
+}  // namespace lane
+}  // namespace armour

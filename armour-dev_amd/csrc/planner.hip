@@ -11,12 +11,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "../../include/armour_hip.h"
 #include "nlp_kernels.hip"
 #include "reach_kernel.hip"
+#include "lane_kernel.hip"
 #include "robots.h"
 
 using namespace armour;
@@ -62,6 +64,10 @@ struct armour_planner {
     // reach
     ReachOut ro;
     ReachArgs ra;
+    // bundle engine (lane_kernel.hip): default; ARMOUR_ENGINE=job selects the per-job reach_kernel
+    bool lane_engine = true;
+    int lane_grid = 0;
+    lane::LaneArgs la;
     // nlp
     NlpDev d;
     int* feas = nullptr;
@@ -167,15 +173,61 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
         HIPCK(hipMemset(p->d_dump, 0, sizeof(double) * p->nops * DUMP_W));
         ra.dump = p->d_dump;
     }
-    ra.arena_cap = 1 << 17;
-    ra.gcap = 1 << 15;
     if ((rc = p->alloc(&p->d_jrs, jobs * NF))) return rc;
-    if ((rc = p->alloc(&ra.arena_h, (size_t)p->reach_grid * ra.arena_cap)) ||
-        (rc = p->alloc(&ra.arena_c, (size_t)p->reach_grid * ra.arena_cap * 3)) ||
-        (rc = p->alloc(&ra.gkh, (size_t)p->reach_grid * ra.gcap)) || (rc = p->alloc(&ra.gki, (size_t)p->reach_grid * ra.gcap)) ||
-        (rc = p->alloc(&ra.gkp, (size_t)p->reach_grid * ra.gcap)) ||
-        (rc = p->alloc(&ra.gout, (size_t)p->reach_grid * ra.gcap * 9)))
-        return rc;
+    {
+        const char* eng = std::getenv("ARMOUR_ENGINE");
+        p->lane_engine = !(eng && std::strcmp(eng, "job") == 0);
+    }
+    if (!p->lane_engine) {
+        ra.arena_cap = 1 << 17;
+        ra.gcap = 1 << 15;
+        if ((rc = p->alloc(&ra.arena_h, (size_t)p->reach_grid * ra.arena_cap)) ||
+            (rc = p->alloc(&ra.arena_c, (size_t)p->reach_grid * ra.arena_cap * 3)) ||
+            (rc = p->alloc(&ra.gkh, (size_t)p->reach_grid * ra.gcap)) || (rc = p->alloc(&ra.gki, (size_t)p->reach_grid * ra.gcap)) ||
+            (rc = p->alloc(&ra.gkp, (size_t)p->reach_grid * ra.gcap)) ||
+            (rc = p->alloc(&ra.gout, (size_t)p->reach_grid * ra.gcap * 9)))
+            return rc;
+    } else {
+        // one resident bundle workgroup per CU, each with its own arena; sizes from the measured
+        // per-job use (~16.5k monomials) times the union inflation, with margin
+        lane::LaneArgs& la = p->la;
+        const long bundles = ((long)Wm * T + lane::LG - 1) / lane::LG;
+        p->lane_grid = (int)(bundles < p->ncu ? bundles : p->ncu);
+        const char* hc = std::getenv("ARMOUR_LANE_HCAP");
+        const char* cc = std::getenv("ARMOUR_LANE_CCAP");
+        la.hcap = hc ? std::atol(hc) : (1L << 16);
+        la.ccap = cc ? std::atol(cc) : (1L << 17);
+        la.gcap = 1 << 15;
+        la.ocap = 4096;
+        int pool = 0;
+        {
+            ProgramBuilder pb;
+            pb.build(p->rp);
+            (void)pb.slot_offsets(&pool);
+        }
+        la.pool_rows = pool + 9;
+        const size_t G = (size_t)p->lane_grid, LGs = lane::LG;
+        if ((rc = p->alloc(&la.pool, G * la.pool_rows * LGs)) || (rc = p->alloc(&la.arena_h, G * la.hcap)) ||
+            (rc = p->alloc(&la.arena_m, G * la.hcap)) || (rc = p->alloc(&la.arena_c, G * la.ccap * LGs)) ||
+            (rc = p->alloc(&la.gkh, G * la.gcap)) || (rc = p->alloc(&la.gki, G * la.gcap)) ||
+            (rc = p->alloc(&la.gkp, G * (la.gcap + 1))) || (rc = p->alloc(&la.ggp, G * (la.gcap + 1))) ||
+            (rc = p->alloc(&la.gout, G * la.ocap * 9 * LGs)) || (rc = p->alloc(&la.gm, G * la.ocap)))
+            return rc;
+        la.prog = p->d_prog;
+        la.nops = p->nops;
+        la.slot_off = p->d_slot_off;
+        la.nslots = p->nslots;
+        la.bytes = p->d_bytes;
+        la.prof = p->d_prof;
+        la.dump = nullptr;
+        if (p->d_dump) {
+            (void)hipFree(p->d_dump);
+            p->allocs.erase(std::find(p->allocs.begin(), p->allocs.end(), (void*)p->d_dump));
+            if ((rc = p->alloc(&p->d_dump, (size_t)p->nops * DUMP_W * lane::LG))) return rc;
+            HIPCK(hipMemset(p->d_dump, 0, sizeof(double) * p->nops * DUMP_W * lane::LG));
+            la.dump = p->d_dump;
+        }
+    }
     // NLP
     NlpDev& d = p->d;
     d.rp = p->d_rp;
@@ -262,7 +314,17 @@ static int run_reach(armour_planner* p) {
     hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, p->stream, p->d_rp, p->W, p->T, p->q0, p->qd0,
                        p->qdd0, p->d_jrs);
     ra.jrs = p->d_jrs;
-    hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, p->stream, p->d_rp, ra, p->ro);
+    if (p->lane_engine) {
+        lane::LaneArgs la = p->la;
+        la.W = p->W;
+        la.T = p->T;
+        la.jrs = p->d_jrs;
+        const long bundles = (jobs + lane::LG - 1) / lane::LG;
+        const int lg = (int)(bundles < p->lane_grid ? bundles : p->lane_grid);
+        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3(lg), dim3(lane::LT), 0, p->stream, p->d_rp, la, p->ro);
+    } else {
+        hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, p->stream, p->d_rp, ra, p->ro);
+    }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(p->ev[4], p->stream));
     const long rows = (long)p->W * d.R;
@@ -514,8 +576,18 @@ int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms
 int armour_get_reach_dump(armour_planner* p, double* dump, int capacity) {
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (!p->d_dump) return fail(ARMOUR_E_STATE, "op dump is off (set ARMOUR_DUMP_OPS before armour_create)");
-    if (dump && capacity >= p->nops)
-        HIPCK(hipMemcpy(dump, p->d_dump, sizeof(double) * DUMP_W * p->nops, hipMemcpyDeviceToHost));
+    if (dump && capacity >= p->nops) {
+        if (p->lane_engine) {
+            // [nops][DUMP_W][64] of bundle 0: lane ARMOUR_DUMP_LANE (default 0) = job of that index
+            const char* ls = std::getenv("ARMOUR_DUMP_LANE");
+            const int l = ls ? std::atoi(ls) & 63 : 0;
+            std::vector<double> all((size_t)p->nops * DUMP_W * lane::LG);
+            HIPCK(hipMemcpy(all.data(), p->d_dump, sizeof(double) * all.size(), hipMemcpyDeviceToHost));
+            for (int k = 0; k < p->nops * DUMP_W; k++) dump[k] = all[(size_t)k * lane::LG + l];
+        } else {
+            HIPCK(hipMemcpy(dump, p->d_dump, sizeof(double) * DUMP_W * p->nops, hipMemcpyDeviceToHost));
+        }
+    }
     return p->nops;
 }
 

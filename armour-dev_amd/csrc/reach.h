@@ -485,6 +485,8 @@ constexpr int DUMP_W = 8;
 #if !defined(__HIP_DEVICE_COMPILE__)
 // host emulation statistics (tests/emu): per op [code, class, term kind, |S0|, |S1|, N, runs, output count]
 inline int* g_op_stats = nullptr;
+// host emulation: per op, the output handle's monomial hashes (structure studies)
+inline void (*g_hash_sink)(int pc, const uint64_t* h, int n) = nullptr;
 #endif
 AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int T, int t, const double* q0,
                     const double* qd0, const double* qdd0, const ReachOut& out, long j, JrsJoint* jrs,
@@ -636,6 +638,11 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
         if (op.sync) x.g.sync();
 #if !defined(__HIP_DEVICE_COMPILE__)
         if (g_op_stats && op.o >= 0) g_op_stats[8 * pc + 7] = x.H[op.o].cnt;
+        if (g_hash_sink)
+            for (int mi = 0; mi < par; mi++) {
+                const int mo = prog[pc + mi].o;
+                if (mo >= 0) g_hash_sink(pc + mi, x.A->h + x.H[mo].hoff, x.H[mo].cnt);
+            }
 #endif
         if (dump) {
             x.g.sync();

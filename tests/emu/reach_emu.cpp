@@ -14,6 +14,7 @@ static int g_unfused = 0;
 extern "C" void emu_set_dump(double* d) { g_dump = d; }
 extern "C" void emu_set_unfused(int u) { g_unfused = u; }
 extern "C" void emu_set_stats(int* st) { armour::g_op_stats = st; }
+extern "C" void emu_set_hash_sink(void (*f)(int, const uint64_t*, int)) { armour::g_hash_sink = f; }
 extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, const double* qdd0,
                          double* link_gens, double* link_center, double* link_rad, int* link_cnt,
                          uint16_t* link_hash, double* link_coef, double* tq_center, double* tq_rad,

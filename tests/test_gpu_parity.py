@@ -86,15 +86,25 @@ def test_config3_batch():
     _compare_batch(200, 40, [21, 22], [np.full(7, -0.4)])
 
 
-def test_batch_position_and_rerun_are_bitwise_stable():
+def test_rerun_bitwise_and_batch_position_stable():
+    """Rerunning a batch is bitwise reproducible. A world's place in the batch changes only the
+    summation order of its pruned amounts: the bundle engine (lane_engine.h) sums them per wave
+    over the bundle's union groups, and which union groups exist depends on the bundle's other
+    jobs. So across positions the values agree to rounding and every decision is identical."""
     T, O = 20, 6
     worlds = [A.make_world(s, O) for s in range(5)]
     P = A.Planner(T=T, max_obstacles=O, max_worlds=5)
     res_a, _ = P.plan(worlds)
     g_a = [P.constraints(w) for w in range(5)]
     res_b, _ = P.plan(worlds[::-1])
+    g_b = [P.constraints(4 - w) for w in range(5)]
     res_c, _ = P.plan(worlds)
     for w in range(5):
-        assert np.array_equal(res_a[w]["k_opt"], res_b[4 - w]["k_opt"])
         assert np.array_equal(res_a[w]["k_opt"], res_c[w]["k_opt"])
         assert np.array_equal(g_a[w], P.constraints(w))
+        assert np.abs(res_a[w]["k_opt"] - res_b[4 - w]["k_opt"]).max() < 1e-8
+        assert res_a[w]["feasible"] == res_b[4 - w]["feasible"]
+        assert res_a[w]["iterations"] == res_b[4 - w]["iterations"]
+        assert np.abs(g_a[w] - g_b[w]).max() < TOL
+        rows = collision_rows(T, O)
+        assert np.array_equal(g_a[w][rows] > COL_THR, g_b[w][rows] > COL_THR)
