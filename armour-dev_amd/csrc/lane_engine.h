@@ -88,6 +88,7 @@ struct LCtx {
     const JrsJoint* jrs;   // this lane's job: jrs[i], i < NF
     unsigned long long* prof;  // optional per-op [cycles, terms] + phase cycles (null: off)
     int nops;
+    int opcode;            // code of the op in flight (phase profile per code)
     long job;              // this lane's job index (clamped into range)
     bool valid;            // lane's job exists (the last bundle may be partial)
 };
@@ -97,7 +98,7 @@ DI void sync() { __syncthreads(); }
 #define LPHASE(k)                                                                                  \
     if (x.prof && x.tid == 0) {                                                                    \
         const long long c_ = clock64();                                                            \
-        atomicAdd(&x.prof[2 * x.nops + (k)], (unsigned long long)(c_ - ph_t));                     \
+        atomicAdd(&x.prof[2 * x.nops + 16 + 8 * x.opcode + (k)], (unsigned long long)(c_ - ph_t));  \
         ph_t = c_;                                                                                 \
     }
 DI long bcast0(long v) {
@@ -573,21 +574,23 @@ struct GMul {
     int na, nb;
     uint32_t nbm;
     double Ac[NA], Bc[NB];
+    DI void ra(int k, double* a, int lane) const { rows<NA>(ca, k, a, lane); }
+    DI void rb(int k, double* b, int lane) const { rows<NB>(cb, k, b, lane); }
     DI void factors(int p, double* a, double* b, int lane) const {
         if (p < na) {
-            rows<NA>(ca, p, a, lane);
+            ra(p, a, lane);
 #pragma unroll
             for (int e = 0; e < NB; e++) b[e] = Bc[e];
         } else if (p < na + nb) {
 #pragma unroll
             for (int e = 0; e < NA; e++) a[e] = Ac[e];
-            rows<NB>(cb, p - na, b, lane);
+            rb(p - na, b, lane);
         } else {
             const int q = p - na - nb;
             const int i = nb == 1 ? q : (int)__umulhi((uint32_t)q, nbm);
             const int j = q - i * nb;
-            rows<NA>(ca, i, a, lane);
-            rows<NB>(cb, j, b, lane);
+            ra(i, a, lane);
+            rb(j, b, lane);
         }
     }
     DI void term(int p, double* v, int lane) const {
@@ -779,7 +782,16 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
     const long hoff = bcast0(ho.hoff);
     int base = 0;
     unsigned long long b = 0;
+    unsigned long long sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long rt = x.prof ? clock64() : 0;
+#define RSTAMP(k)                                                                                  \
+    if (x.prof && x.tid == 0) {                                                                    \
+        const long long c_ = clock64();                                                            \
+        sub[k] += (unsigned long long)(c_ - rt);                                                   \
+        rt = c_;                                                                                   \
+    }
     for (int r0 = 0, par = 0; r0 < NG; r0 += RG, par ^= 1) {
+        RSTAMP(7)
         int lo[U], sz[U];
         int maxsz = 0;
 #pragma unroll
@@ -790,6 +802,9 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
             sz[u] = in ? ui(gp[g + 1]) - lo[u] : 0;
             maxsz = sz[u] > maxsz ? sz[u] : maxsz;
         }
+        RSTAMP(0)
+        sub[5] += 1;
+        sub[6] += maxsz;
         double acc[U][NV];
 #pragma unroll
         for (int u = 0; u < U; u++) G.term(ui((int)ki[lo[u]]), acc[u], x.lane);
@@ -814,7 +829,9 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
             mk[u] = ballot(keep);
             if (x.lane == 0) x.rmask[par * 64 + x.wave * U + u] = mk[u];
         }
+        RSTAMP(1)
         sync();
+        RSTAMP(2)
         const unsigned long long km = ballot(x.lane < RG && r0 + x.lane < NG && x.rmask[par * 64 + x.lane] != 0);
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -830,7 +847,11 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
             }
         }
         base += __popcll(km);
+        RSTAMP(3)
     }
+#undef RSTAMP
+    if (x.prof && x.tid == 0)
+        for (int k = 0; k < 8; k++) atomicAdd(&x.prof[2 * x.nops + k], sub[k]);
     if (b) atomicAdd(&x.A->bytes, b);
     LPHASE(4)
     sync();
@@ -1361,6 +1382,7 @@ DI void run_program(LCtx& x, const RobotParams& rp, const Op* prog, int nops, co
         const int par = op.par > 1 ? op.par : 1;
         const long long c0 = (x.prof && x.tid == 0) ? clock64() : 0;
         int nterms = 0;
+        x.opcode = op.code;
         switch (op.code) {
             case OP_JRS: break;  // this lane's JRS scalars are read from jrs_kernel's output in place
             case OP_MAKE1D:

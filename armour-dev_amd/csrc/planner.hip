@@ -145,8 +145,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
         HIPCK(hipMemcpy(p->d_prog, pb.ops.data(), sizeof(Op) * pb.ops.size(), hipMemcpyHostToDevice));
         HIPCK(hipMemcpy(p->d_slot_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
         if (std::getenv("ARMOUR_PROFILE_OPS")) {
-            if ((rc = p->alloc(&p->d_prof, 2 * pb.ops.size() + 16))) return rc;
-            HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 16)));
+            if ((rc = p->alloc(&p->d_prof, 2 * pb.ops.size() + 16 + 8 * OP_NCODES))) return rc;
+            HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 16 + 8 * OP_NCODES)));
         }
     }
     // reach workspace: four resident workgroups per CU, each with a private arena
@@ -568,8 +568,12 @@ int armour_get_torque_radius(armour_planner* p, int w, double* radius) {
 int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms, int capacity) {
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (!p->d_prof) return fail(ARMOUR_E_STATE, "op profiling is off (set ARMOUR_PROFILE_OPS before armour_create)");
-    if (cycles_terms && capacity >= p->nops + 8)
-        HIPCK(hipMemcpy(cycles_terms, p->d_prof, sizeof(unsigned long long) * (2 * p->nops + 16), hipMemcpyDeviceToHost));
+    // capacity in pairs: nops + 8 -> per-op [cycles, terms] + 16 phase totals; nops + 8 + 4 * OP_NCODES
+    // adds the bundle engine's phase cycles per op code [OP_NCODES][8]
+    if (cycles_terms && capacity >= p->nops + 8) {
+        const size_t n = capacity >= p->nops + 8 + 4 * OP_NCODES ? 2 * p->nops + 16 + 8 * OP_NCODES : 2 * p->nops + 16;
+        HIPCK(hipMemcpy(cycles_terms, p->d_prof, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    }
     return p->nops;
 }
 
