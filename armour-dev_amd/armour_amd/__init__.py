@@ -57,6 +57,9 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         L.armour_create.restype = ctypes.c_void_p
         L.armour_create.argtypes = [ctypes.POINTER(Config)]
+        L.armour_create_robot.restype = ctypes.c_void_p
+        L.armour_create_robot.argtypes = [ctypes.POINTER(Config), ctypes.c_void_p]
+        L.armour_robot_builtin.argtypes = [ctypes.c_int, ctypes.c_void_p]
         L.armour_destroy.argtypes = [ctypes.c_void_p]
         L.armour_last_error.restype = ctypes.c_char_p
         L.armour_num_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -77,7 +80,7 @@ def lib():
 
 
 # every symbol include/armour_hip.h declares (checked by tests/test_abi.py)
-ABI_SYMBOLS = ["armour_create", "armour_destroy", "armour_last_error", "armour_num_constraints",
+ABI_SYMBOLS = ["armour_create", "armour_create_robot", "armour_robot_builtin", "armour_destroy", "armour_last_error", "armour_num_constraints",
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
@@ -96,9 +99,15 @@ def _ptr(a):
 class Planner:
     """Batched MI355X planner. A world is (q0, qd0, qdd0, q_des, obstacles[O, 12])."""
 
-    def __init__(self, T=100, max_obstacles=20, max_worlds=1, device=0, max_iter=0):
+    def __init__(self, T=100, max_obstacles=20, max_worlds=1, device=0, max_iter=0, robot=None):
+        """robot: None (built-in Kinova Gen3 tables) or a robot-table dict (armour_amd.robot_tables)"""
         cfg = Config(0, T, max_obstacles, max_worlds, device, max_iter)
-        self.h = lib().armour_create(ctypes.byref(cfg))
+        if robot is None:
+            self.h = lib().armour_create(ctypes.byref(cfg))
+        else:
+            from .robot_tables import to_struct
+            self._robot = to_struct(robot)
+            self.h = lib().armour_create_robot(ctypes.byref(cfg), ctypes.byref(self._robot))
         if not self.h:
             raise ArmourError(f"armour_create failed: {lib().armour_last_error().decode()}")
         self.T = T

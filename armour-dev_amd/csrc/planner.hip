@@ -90,9 +90,9 @@ struct armour_planner {
     }
 };
 
-static int planner_init(armour_planner* p, const armour_config* cfg) {
+static int planner_init(armour_planner* p, const armour_config* cfg, const armour_robot* robot) {
     p->cfg = *cfg;
-    if (cfg->robot != 0) return fail(ARMOUR_E_ARG, "unknown robot id");
+    if (!robot && cfg->robot != 0) return fail(ARMOUR_E_ARG, "unknown robot id");
     if (cfg->num_time_steps <= 0 || (cfg->num_time_steps % 2) != 0)
         return fail(ARMOUR_E_ARG, "num_time_steps must be a positive even number (KPR/Parameters.h:16)");
     if (cfg->max_obstacles < 0 || cfg->max_obstacles > MAX_OBS || cfg->max_worlds <= 0)
@@ -101,7 +101,12 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
     int dev = 0;
     HIPCK(hipGetDevice(&dev));
     HIPCK(hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    kinova_gen3(p->rp);
+    if (robot) {
+        if (!robot_from_tables(*robot, p->rp))
+            return fail(ARMOUR_E_ARG, "invalid robot tables (num_joints 7..9, actuated joints first, M_min > 0, K > 0)");
+    } else {
+        kinova_gen3(p->rp);
+    }
     p->T = cfg->num_time_steps;
     p->NJ = p->rp.num_joints;
     p->Omax = cfg->max_obstacles;
@@ -135,8 +140,17 @@ static int planner_init(armour_planner* p, const armour_config* cfg) {
         pb.build(p->rp);
         int pool = 0;
         const std::vector<int> off = pb.slot_offsets(&pool);
-        if (pb.nslots > MAX_SLOTS || pool > POOL_DOUBLES)
-            return fail(ARMOUR_E_CAPACITY, "reach program needs more handle slots / payload pool than the kernel has");
+        {
+            const char* eng = std::getenv("ARMOUR_ENGINE");
+            const bool job_engine = eng && std::strcmp(eng, "job") == 0;
+            // the bundle engine's payload pool lives in HBM, sized below; the per-job engine's in LDS
+            if (pb.nslots > MAX_SLOTS || (job_engine && pool > POOL_DOUBLES)) {
+                char buf[200];
+                std::snprintf(buf, sizeof(buf), "reach program needs %d handle slots (kernel: %d) and %d payload doubles (per-job engine: %d)",
+                              pb.nslots, MAX_SLOTS, pool, POOL_DOUBLES);
+                return fail(ARMOUR_E_CAPACITY, buf);
+            }
+        }
         p->nops = (int)pb.ops.size();
         p->nslots = pb.nslots;
         if ((rc = p->alloc(&p->d_prog, pb.ops.size())) || (rc = p->alloc(&p->d_bytes, 1)) ||
@@ -399,10 +413,20 @@ extern "C" {
 
 const char* armour_last_error(void) { return g_err.c_str(); }
 
-armour_planner* armour_create(const armour_config* cfg) {
+int armour_robot_builtin(int robot_id, armour_robot* out) {
+    if (!out || robot_id != 0) return fail(ARMOUR_E_ARG, "unknown robot id / null output");
+    RobotParams r;
+    kinova_gen3(r);
+    robot_to_tables(r, *out);
+    return 0;
+}
+
+armour_planner* armour_create(const armour_config* cfg) { return armour_create_robot(cfg, nullptr); }
+
+armour_planner* armour_create_robot(const armour_config* cfg, const armour_robot* robot) {
     if (!cfg) { fail(ARMOUR_E_ARG, "null config"); return nullptr; }
     armour_planner* p = new armour_planner();
-    if (planner_init(p, cfg) != 0) {
+    if (planner_init(p, cfg, robot) != 0) {
         std::string keep = g_err;
         armour_destroy(p);
         g_err = keep;

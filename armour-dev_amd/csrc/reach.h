@@ -190,7 +190,7 @@ struct Op {
     double s;
 };
 
-constexpr int MAX_SLOTS = 76;
+constexpr int MAX_SLOTS = 96;
 
 // thread-0 bodies are inlined too: an out-of-line variant (stack arrays passed through a lambda
 // into a nested out-of-line call) was miscompiled for gfx950 — tools/dump_ops.py localised it to

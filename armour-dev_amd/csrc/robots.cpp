@@ -3,6 +3,7 @@
 // KPR/Parameters.h:10-59. RPY rotation matrices are pre-computed here with the reference's own
 // closed form (PZsparse.cu:160-176) so device code needs no trigonometry for them.
 #include "robots.h"
+#include "../../include/armour_hip.h"
 #include <cmath>
 #include <cstring>
 
@@ -86,15 +87,102 @@ void kinova_gen3(RobotParams& r) {
     r.qde = 2 * r.eps;
     r.qdae = r.eps;
     r.qddae = 2 * r.K * r.eps;
+    planner_defaults(r);
+    finalize_params(r);
+}
+
+void planner_defaults(RobotParams& r) {
     // planner parameters (Parameters.h)
     r.duration = 1.0;
     r.simplify_threshold = 5e-4;
-    for (int i = 0; i < 7; i++) r.k_range[i] = M_PI / 48;
+    for (int i = 0; i < NF; i++) r.k_range[i] = M_PI / 48;
     r.collision_violation = 1e-4;
     r.torque_violation = 1e-2;
     r.cost_scale = 10.0;
     r.t_plan = 0.5;
+}
+
+bool robot_from_tables(const armour_robot& t, RobotParams& r) {
+    if (t.num_joints < NF || t.num_joints > MAX_J) return false;
+    std::memset(&r, 0, sizeof(r));
+    r.num_joints = t.num_joints;
+    for (int i = 0; i < t.num_joints; i++) {
+        if (t.axes[i] < -3 || t.axes[i] > 3) return false;
+        if (i < NF && t.axes[i] == 0) return false;  // the actuated joints come first
+        r.axes[i] = t.axes[i];
+    }
+    std::memcpy(r.trans, t.trans, sizeof(r.trans));
+    std::memcpy(r.rots, t.rots, sizeof(r.rots));
+    std::memcpy(r.mass, t.mass, sizeof(r.mass));
+    std::memcpy(r.com, t.com, sizeof(r.com));
+    std::memcpy(r.inertia, t.inertia, sizeof(r.inertia));
+    r.mass_uncertainty = t.mass_uncertainty;
+    r.inertia_uncertainty = t.inertia_uncertainty;
+    std::memcpy(r.friction, t.friction, sizeof(r.friction));
+    std::memcpy(r.damping, t.damping, sizeof(r.damping));
+    std::memcpy(r.armature, t.armature, sizeof(r.armature));
+    for (int i = 0; i < NF; i++) {
+        r.state_lb[i] = t.state_lb[i];
+        r.state_ub[i] = t.state_ub[i];
+        r.speed_limits[i] = t.speed_limits[i];
+        r.torque_limits[i] = t.torque_limits[i];
+        r.wrap_mask[i] = t.wrap[i] ? 1 : 0;
+    }
+    r.gravity = t.gravity;
+    for (int i = 0; i < MAX_J; i++)
+        for (int e = 0; e < 3; e++) {
+            r.link_c[i][e] = t.link_center[3 * i + e];
+            r.link_g[i][e] = t.link_generators[3 * i + e];
+        }
+    r.alpha = t.alpha;
+    r.V_m = t.V_m;
+    r.M_max = t.M_max;
+    r.M_min = t.M_min;
+    r.K = t.K;
+    if (!(r.M_min > 0) || !(r.K > 0) || !(r.V_m >= 0)) return false;
+    // derived bounds as the reference's header computes them (KinovaWithoutGripperInfo.h:102-112)
+    r.eps = std::sqrt(2 * r.V_m / r.M_min);
+    r.qe = r.eps / r.K;
+    r.qde = 2 * r.eps;
+    r.qdae = r.eps;
+    r.qddae = 2 * r.K * r.eps;
+    planner_defaults(r);
     finalize_params(r);
+    return true;
+}
+
+void robot_to_tables(const RobotParams& r, armour_robot& t) {
+    std::memset(&t, 0, sizeof(t));
+    t.num_joints = r.num_joints;
+    for (int i = 0; i < MAX_J; i++) t.axes[i] = r.axes[i];
+    std::memcpy(t.trans, r.trans, sizeof(t.trans));
+    std::memcpy(t.rots, r.rots, sizeof(t.rots));
+    std::memcpy(t.mass, r.mass, sizeof(t.mass));
+    std::memcpy(t.com, r.com, sizeof(t.com));
+    std::memcpy(t.inertia, r.inertia, sizeof(t.inertia));
+    t.mass_uncertainty = r.mass_uncertainty;
+    t.inertia_uncertainty = r.inertia_uncertainty;
+    std::memcpy(t.friction, r.friction, sizeof(t.friction));
+    std::memcpy(t.damping, r.damping, sizeof(t.damping));
+    std::memcpy(t.armature, r.armature, sizeof(t.armature));
+    for (int i = 0; i < NF; i++) {
+        t.state_lb[i] = r.state_lb[i];
+        t.state_ub[i] = r.state_ub[i];
+        t.speed_limits[i] = r.speed_limits[i];
+        t.torque_limits[i] = r.torque_limits[i];
+        t.wrap[i] = r.wrap_mask[i];
+    }
+    t.gravity = r.gravity;
+    for (int i = 0; i < MAX_J; i++)
+        for (int e = 0; e < 3; e++) {
+            t.link_center[3 * i + e] = r.link_c[i][e];
+            t.link_generators[3 * i + e] = r.link_g[i][e];
+        }
+    t.alpha = r.alpha;
+    t.V_m = r.V_m;
+    t.M_max = r.M_max;
+    t.M_min = r.M_min;
+    t.K = r.K;
 }
 
 }  // namespace armour

@@ -37,10 +37,13 @@ def parse():
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--O", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
+    ap.add_argument("--robot", default="kinova", choices=["kinova", "fetch"],
+                    help="kinova: built-in Gen3 tables (configs 1-4); fetch: tests/golden/robot_fetch.json, the "
+                         "Fetch arm from its URDF (config 5, at fp64)")
     return ap.parse_args()
 
 
-def cpu_baseline(worlds, T, seconds):
+def cpu_baseline(worlds, T, seconds, robot=None):
     """Oracle (CPU restatement of the reference path, oracle/) on the host cores: whole plans of
     the same worlds until `seconds` of work, OpenMP threads = the box's CPU share (<= 16)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -49,7 +52,7 @@ def cpu_baseline(worlds, T, seconds):
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     done, t0 = 0, time.perf_counter()
     for w in worlds:
-        P = OraclePlanner(*w, T=T, threads=threads)
+        P = OraclePlanner(*w, T=T, threads=threads, robot=robot)
         P.reach()
         P.plan()
         done += 1
@@ -105,8 +108,14 @@ def main():
     from armour_amd import dist as D
 
     # weak scaling: rank r plans worlds r*batch .. r*batch+batch-1 (armour_amd.dist.shard of the whole job)
-    worlds = [A.make_world(i, a.O) for i in D.shard(a.batch * world_size, rank, world_size)]
-    planner = A.Planner(T=a.T, max_obstacles=a.O, max_worlds=a.batch, device=local_rank)
+    robot, geo, robot_name = None, A.KINOVA, "Kinova Gen3 7-DOF"
+    if a.robot == "fetch":
+        from armour_amd import robot_tables as RT
+        robot = RT.load_json(os.path.join(ROOT, "tests", "golden", "robot_fetch.json"))
+        geo = RT.geometry(robot)
+        robot_name = "Fetch arm (URDF, 7 actuated + fixed gripper)"
+    worlds = [A.make_world(i, a.O, robot=geo) for i in D.shard(a.batch * world_size, rank, world_size)]
+    planner = A.Planner(T=a.T, max_obstacles=a.O, max_worlds=a.batch, device=local_rank, robot=robot)
 
     def gather(res):
         return D.gather(D.records(res), dist, device="cuda" if dist is not None else None)
@@ -159,7 +168,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic random-obstacle worlds (armour_amd.worlds, seeds rank*batch+i)",
-        "config": {"workload": f"Kinova Gen3 7-DOF, T={a.T}, O={a.O} box obstacles, {a.batch} worlds/GPU/step",
+        "config": {"workload": f"{robot_name}, T={a.T}, O={a.O} box obstacles, {a.batch} worlds/GPU/step",
                    "num_time_steps": a.T, "obstacles": a.O, "worlds_per_gpu": a.batch,
                    "parallelism": f"world-sharded x{world_size}, RCCL all_gather of per-world records"},
         "breakdown_ms": {"reach": float(np.mean([t["reach_ms"] for t in tms])),
@@ -172,12 +181,16 @@ def main():
                      "algorithmic_bytes_per_launch": rk_bytes, "launch_ms": rk_ms},
         "cpu_baseline": None,
     }
-    tr = traffic_record(a.T, a.O, a.batch)
+    tr = traffic_record(a.T, a.O, a.batch) if a.robot == "kinova" else None
     if tr is not None:
         line["roofline"]["traffic"] = tr[1]["traffic_bytes_per_launch"]
         line["roofline"]["traffic_source"] = os.path.relpath(tr[0], ROOT)
     if a.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(worlds, a.T, a.cpu_seconds)
+        rs = None
+        if robot is not None:
+            from armour_amd import robot_tables as RT
+            rs = RT.to_struct(robot)
+        line["cpu_baseline"] = cpu_baseline(worlds, a.T, a.cpu_seconds, robot=rs)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

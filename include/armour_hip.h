@@ -72,6 +72,38 @@ typedef struct armour_timing {
 
 armour_planner* armour_create(const armour_config* cfg);
 void armour_destroy(armour_planner* p);
+
+/* Robot tables: the content of the reference's compile-time robot header (Kinova:
+ * KPR/KinovaWithoutGripperInfo.h:10-112; Fetch: ACMP/FetchInfo.h:8-107) as run-time data, so a
+ * robot is data rather than a rebuild. Joint i rotates about axis |axes[i]| (1 x, 2 y, 3 z; negative:
+ * reversed; 0: fixed) after the frame offset trans[i] / rots[i] (URDF joint origin xyz / rpy);
+ * link i (the child of joint i) has mass, centre of mass, inertia (row-major 3x3) and a box
+ * zonotope (centre, half extents: the STL bounding box of create_pz_bounding_boxes.m). The first
+ * ARMOUR_NUM_FACTORS joints are the actuated ones. armour_amd/robot_tables.py builds these from a
+ * URDF and its meshes. */
+#define ARMOUR_MAX_JOINTS 9
+typedef struct armour_robot {
+    int num_joints;                               /* NUM_JOINTS, 7..9 */
+    int axes[ARMOUR_MAX_JOINTS];
+    int wrap[ARMOUR_NUM_FACTORS];                 /* continuous joints: cost term wrapped to [-pi, pi] */
+    double trans[(ARMOUR_MAX_JOINTS + 1) * 3];
+    double rots[ARMOUR_MAX_JOINTS * 3];
+    double mass[ARMOUR_MAX_JOINTS];
+    double com[ARMOUR_MAX_JOINTS * 3];
+    double inertia[ARMOUR_MAX_JOINTS * 9];
+    double mass_uncertainty, inertia_uncertainty;
+    double friction[ARMOUR_MAX_JOINTS], damping[ARMOUR_MAX_JOINTS], armature[ARMOUR_MAX_JOINTS];
+    double state_lb[ARMOUR_NUM_FACTORS], state_ub[ARMOUR_NUM_FACTORS];  /* +-1000: continuous */
+    double speed_limits[ARMOUR_NUM_FACTORS], torque_limits[ARMOUR_NUM_FACTORS];
+    double gravity;
+    double link_center[ARMOUR_MAX_JOINTS * 3], link_generators[ARMOUR_MAX_JOINTS * 3];
+    double alpha, V_m, M_max, M_min, K;           /* ultimate bound of the robust controller */
+} armour_robot;
+
+/* built-in tables (robot id 0: Kinova Gen3 without gripper); 0 / ARMOUR_E_ARG */
+int armour_robot_builtin(int robot_id, armour_robot* out);
+/* armour_create with the given robot tables (cfg->robot is ignored) */
+armour_planner* armour_create_robot(const armour_config* cfg, const armour_robot* robot);
 const char* armour_last_error(void);
 
 /* constraints of a world with O obstacles: 7T + 7*T*O + 28  (KPR/NLPclass.cu:47-49) */

@@ -30,6 +30,8 @@ def lib():
         L = ctypes.CDLL(path)
         L.oracle_create.restype = ctypes.c_void_p
         L.oracle_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int] + [_dp] * 5 + [ctypes.c_int]
+        L.oracle_create_robot.restype = ctypes.c_void_p
+        L.oracle_create_robot.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [_dp] * 5 + [ctypes.c_int]
         L.oracle_free.argtypes = [ctypes.c_void_p]
         L.oracle_reach.restype = ctypes.c_double
         L.oracle_reach.argtypes = [ctypes.c_void_p]
@@ -51,14 +53,21 @@ def lib():
 class OraclePlanner:
     """One planning problem on the CPU oracle (KPR/armour_main.cu semantics)."""
 
-    def __init__(self, q0, qd0, qdd0, q_des, obstacles, T=100, threads=1, robot_id=0, num_joints=7):
+    def __init__(self, q0, qd0, qdd0, q_des, obstacles, T=100, threads=1, robot_id=0, num_joints=7, robot=None):
+        """robot: None (Kinova tables) or a ctypes structure in the armour_robot layout
+        (include/armour_hip.h; armour_amd.robot_tables.to_struct builds one)"""
         self.T = T
-        self.NJ = num_joints
+        self.NJ = int(robot.num_joints) if robot is not None else num_joints
         obstacles = np.ascontiguousarray(np.asarray(obstacles, dtype=np.float64).reshape(-1, 12))
         self.O = obstacles.shape[0]
         arrs = [np.ascontiguousarray(np.asarray(a, dtype=np.float64)) for a in (q0, qd0, qdd0, q_des)]
         obs = obstacles if self.O > 0 else np.zeros((1, 12))
-        self.h = lib().oracle_create(robot_id, T, self.O, *[_ptr(a) for a in arrs], _ptr(obs), threads)
+        if robot is None:
+            self.h = lib().oracle_create(robot_id, T, self.O, *[_ptr(a) for a in arrs], _ptr(obs), threads)
+        else:
+            self._robot = robot
+            self.h = lib().oracle_create_robot(ctypes.byref(robot), T, self.O, *[_ptr(a) for a in arrs], _ptr(obs),
+                                               threads)
         if not self.h:
             raise ValueError("oracle_create failed")
         self.m = lib().oracle_num_constraints(self.h)

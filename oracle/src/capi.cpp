@@ -1,6 +1,7 @@
 // ORACLE — TEST INFRASTRUCTURE ONLY. Never linked into the product.
 // C entry points of the CPU oracle, loaded by tests/ and bench.py's cpu_baseline leg via ctypes.
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <vector>
 #include "ipm.h"
@@ -29,6 +30,68 @@ Robot robot_by_id(int id) {
     (void)id;
     return kinova_without_gripper();
 }
+
+// robot tables in the layout of include/armour_hip.h armour_robot (the tests hand the same bytes to
+// the product and to this checker)
+constexpr int RD_J = 9;
+struct RobotDesc {
+    int num_joints;
+    int axes[RD_J];
+    int wrap[NF];
+    double trans[(RD_J + 1) * 3];
+    double rots[RD_J * 3];
+    double mass[RD_J];
+    double com[RD_J * 3];
+    double inertia[RD_J * 9];
+    double mass_uncertainty, inertia_uncertainty;
+    double friction[RD_J], damping[RD_J], armature[RD_J];
+    double state_lb[NF], state_ub[NF];
+    double speed_limits[NF], torque_limits[NF];
+    double gravity;
+    double link_center[RD_J * 3], link_generators[RD_J * 3];
+    double alpha, V_m, M_max, M_min, K;
+};
+
+Robot robot_from_desc(const RobotDesc& t) {
+    Robot r{};
+    r.num_joints = t.num_joints;
+    for (int i = 0; i < RD_J; i++) {
+        r.axes[i] = t.axes[i];
+        r.mass[i] = t.mass[i];
+        r.friction[i] = t.friction[i];
+        r.damping[i] = t.damping[i];
+        r.armature[i] = t.armature[i];
+        for (int e = 0; e < 3; e++) {
+            r.rots[3 * i + e] = t.rots[3 * i + e];
+            r.com[3 * i + e] = t.com[3 * i + e];
+            r.link_c[i][e] = t.link_center[3 * i + e];
+            r.link_g[i][e] = t.link_generators[3 * i + e];
+        }
+        for (int e = 0; e < 9; e++) r.inertia[9 * i + e] = t.inertia[9 * i + e];
+    }
+    for (int e = 0; e < (RD_J + 1) * 3; e++) r.trans[e] = t.trans[e];
+    r.mass_uncertainty = t.mass_uncertainty;
+    r.inertia_uncertainty = t.inertia_uncertainty;
+    for (int i = 0; i < NF; i++) {
+        r.state_lb[i] = t.state_lb[i];
+        r.state_ub[i] = t.state_ub[i];
+        r.speed_limits[i] = t.speed_limits[i];
+        r.torque_limits[i] = t.torque_limits[i];
+        r.wrap_mask[i] = t.wrap[i] ? 1 : 0;
+    }
+    r.gravity = t.gravity;
+    r.alpha = t.alpha;
+    r.V_m = t.V_m;
+    r.M_max = t.M_max;
+    r.M_min = t.M_min;
+    r.K = t.K;
+    r.eps = std::sqrt(2 * r.V_m / r.M_min);  // KinovaWithoutGripperInfo.h:102-112
+    r.qe = r.eps / r.K;
+    r.qde = 2 * r.eps;
+    r.qdae = r.eps;
+    r.qddae = 2 * r.K * r.eps;
+    return r;
+}
 }  // namespace
 
 extern "C" {
@@ -37,6 +100,20 @@ void* oracle_create(int robot_id, int T, int O, const double* q0, const double* 
                     const double* q_des, const double* obstacles, int threads) {
     try {
         Robot r = robot_by_id(robot_id);
+        Params p = default_params(T);
+        Planner* P = new Planner(r, p, q0, qd0, qdd0, q_des, O, obstacles);
+        P->num_threads = threads > 0 ? threads : 1;
+        return P;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+// the same with robot tables (RobotDesc = armour_robot layout)
+void* oracle_create_robot(const void* robot, int T, int O, const double* q0, const double* qd0, const double* qdd0,
+                          const double* q_des, const double* obstacles, int threads) {
+    try {
+        Robot r = robot_from_desc(*static_cast<const RobotDesc*>(robot));
         Params p = default_params(T);
         Planner* P = new Planner(r, p, q0, qd0, qdd0, q_des, O, obstacles);
         P->num_threads = threads > 0 ? threads : 1;

@@ -8,13 +8,17 @@ solver's k_opt 1e-8 with identical iteration counts and feasibility; every colli
 import numpy as np
 import pytest
 
+import os
+
 import armour_amd as A
+from armour_amd import robot_tables as RT
 from conftest import golden_names, load_golden, world_of
 from oracle import OraclePlanner
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-9
 COL_THR = 1e-4  # COLLISION_AVOIDANCE_CONSTRAINT_VIOLATION_THRESHOLD (Parameters.h:38)
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def collision_rows(T, O):
@@ -50,13 +54,14 @@ def test_fixture(name):
     assert tm["reach_kernel_ms"] > 0 and tm["reach_bytes"] > 0
 
 
-def _compare_batch(T, O, seeds, xs):
-    worlds = [A.make_world(s, O) for s in seeds]
-    P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
+def _compare_batch(T, O, seeds, xs, robot=None):
+    geo = RT.geometry(robot) if robot is not None else A.KINOVA
+    worlds = [A.make_world(s, O, robot=geo) for s in seeds]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds), robot=robot)
     P.reach(worlds)
     refs = []
     for w, world in enumerate(worlds):
-        R = OraclePlanner(*world, T=T, threads=8)
+        R = OraclePlanner(*world, T=T, threads=8, robot=RT.to_struct(robot) if robot is not None else None)
         R.reach()
         refs.append(R)
         np.testing.assert_allclose(P.torque_radius(w), R.torque_radius(), rtol=0, atol=TOL)
@@ -79,6 +84,14 @@ def _compare_batch(T, O, seeds, xs):
 def test_config2_batch():
     """BASELINE configs[1]: Kinova, T=100, O=20"""
     _compare_batch(100, 20, [11, 12, 13, 14], [np.zeros(7), np.array([0.5, 0.6, 0.7, 0.0, -0.5, -0.6, -0.7])])
+
+
+def test_config5_fetch_batch():
+    """BASELINE configs[4]: the Fetch arm from its URDF (tests/golden/robot_fetch.json: 7 actuated
+    joints + the fixed gripper), here at fp64 and reduced sizes (T=40, O=8); the full-size run is
+    `bench.py --robot fetch`"""
+    fetch = RT.load_json(os.path.join(GOLD, "robot_fetch.json"))
+    _compare_batch(40, 8, [31, 32, 33], [np.zeros(7), np.linspace(-0.6, 0.6, 7)], robot=fetch)
 
 
 def test_config3_batch():
