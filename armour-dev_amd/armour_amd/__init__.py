@@ -60,6 +60,7 @@ def lib():
         L.armour_create_robot.restype = ctypes.c_void_p
         L.armour_create_robot.argtypes = [ctypes.POINTER(Config), ctypes.c_void_p]
         L.armour_robot_builtin.argtypes = [ctypes.c_int, ctypes.c_void_p]
+        L.armour_device_compute_units.argtypes = [ctypes.c_int]
         L.armour_destroy.argtypes = [ctypes.c_void_p]
         L.armour_last_error.restype = ctypes.c_char_p
         L.armour_num_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -80,11 +81,19 @@ def lib():
 
 
 # every symbol include/armour_hip.h declares (checked by tests/test_abi.py)
-ABI_SYMBOLS = ["armour_create", "armour_create_robot", "armour_robot_builtin", "armour_destroy", "armour_last_error", "armour_num_constraints",
+ABI_SYMBOLS = ["armour_create", "armour_create_robot", "armour_robot_builtin", "armour_device_compute_units", "armour_destroy", "armour_last_error", "armour_num_constraints",
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
                "armour_get_reach_dump"]
+
+
+def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
+    """worlds per step that fill `waves` whole bundle waves of the device (lane_kernel.hip runs one
+    64-job bundle per CU at a time): floor(waves * CUs * 64 / T)"""
+    n = lib().armour_device_compute_units(device)
+    _check(min(0, n))
+    return max(1, (waves * n * 64) // T)
 
 
 def _check(rc):
@@ -222,4 +231,4 @@ class Planner:
         return r
 
 
-__all__ = ["Planner", "ArmourError", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]
+__all__ = ["Planner", "ArmourError", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]

@@ -413,6 +413,13 @@ extern "C" {
 
 const char* armour_last_error(void) { return g_err.c_str(); }
 
+int armour_device_compute_units(int device) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+        return fail(ARMOUR_E_HIP, "hipDeviceGetAttribute failed (no device?)");
+    return n;
+}
+
 int armour_robot_builtin(int robot_id, armour_robot* out) {
     if (!out || robot_id != 0) return fail(ARMOUR_E_ARG, "unknown robot id / null output");
     RobotParams r;

@@ -4,7 +4,7 @@
 Metric (BASELINE.json): planning iterations/sec at 1/2/4/8 GPUs. One planning iteration = one
 complete plan of KPR/armour_main.cu (JRS -> PZ FK/RNEA -> torque radius -> hyperplanes -> NLP to
 termination -> feasibility re-check). A step = one batch of `--batch` synthetic random-obstacle
-worlds planned on each GPU (weak scaling: every rank plans its own worlds); after each step the
+worlds planned on each GPU (default: two whole waves of 64-job reach bundles) (weak scaling: every rank plans its own worlds); after each step the
 per-world records (k_opt, cost, feasible) are all-gathered over RCCL and rank 0 takes the argmin
 over feasible worlds (the only collective on this path).
 
@@ -33,7 +33,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=256, help="worlds per GPU per step")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="worlds per GPU per step (0: two whole bundle waves of the device, floor(2 * CUs * 64 / T): "
+                         "327 on MI355X at T=100)")
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--O", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
@@ -106,6 +108,9 @@ def main():
 
     import armour_amd as A
     from armour_amd import dist as D
+
+    if a.batch <= 0:
+        a.batch = A.default_batch(a.T, local_rank)
 
     # weak scaling: rank r plans worlds r*batch .. r*batch+batch-1 (armour_amd.dist.shard of the whole job)
     robot, geo, robot_name = None, A.KINOVA, "Kinova Gen3 7-DOF"

@@ -100,6 +100,10 @@ typedef struct armour_robot {
     double alpha, V_m, M_max, M_min, K;           /* ultimate bound of the robust controller */
 } armour_robot;
 
+/* compute units of a HIP device (< 0: error). The reach kernel runs one 64-job bundle per CU at a
+ * time, so batches of whole bundle waves, W = k * CUs * 64 / num_time_steps worlds, fill the chip. */
+int armour_device_compute_units(int device);
+
 /* built-in tables (robot id 0: Kinova Gen3 without gripper); 0 / ARMOUR_E_ARG */
 int armour_robot_builtin(int robot_id, armour_robot* out);
 /* armour_create with the given robot tables (cfg->robot is ignored) */

@@ -3,7 +3,7 @@ corrected as MI355X_MICROARCH.md §HBM prescribes: both counters are in KiB; on 
 reports half the bytes of a wide coalesced read, so it is doubled.
 
 usage: python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv>
-                                   <kernel-substring> <out.json> [round]
+                                   <kernel-substring> <out.json> [round] [batch]
 The record carries the workload (bench.py defaults) and the sha1 of the library build it measured,
 so bench.py only reports it for that exact build.
 """
@@ -25,6 +25,7 @@ def per_dispatch(path, counter, kernel):
 def main():
     fpath, wpath, kernel, out = sys.argv[1:5]
     rnd = sys.argv[5] if len(sys.argv) > 5 else "r01"
+    batch = int(sys.argv[6]) if len(sys.argv) > 6 else 327  # bench.py's default on MI355X (256 CUs, T=100)
     fetch = per_dispatch(fpath, "FETCH_SIZE", kernel)
     write = per_dispatch(wpath, "WRITE_SIZE", kernel)
     if not fetch or not write:
@@ -34,7 +35,7 @@ def main():
     res = dict(kernel=kernel, launches=[len(fetch), len(write)], fetch_size_kib=f_kib, write_size_kib=w_kib,
                traffic_bytes_per_launch=(2 * f_kib + w_kib) * 1024,
                correction="bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM)",
-               config=dict(T=100, O=20, batch=256), round=rnd,
+               config=dict(T=100, O=20, batch=batch), round=rnd,
                command="rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE --output-format csv -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0")
     import hashlib
     import os
