@@ -24,10 +24,14 @@ namespace lane {
 constexpr int LG = 64;  // jobs per bundle = lanes per wave
 
 #ifndef LANE_CFG_WAVES
-#define LANE_CFG_WAVES 8
+#define LANE_CFG_WAVES 4
 #define LANE_CFG_KEYS 2048
 #define LANE_CFG_STAGE 2048
 #endif
+#ifndef LANE_CFG_WG_PER_CU
+#define LANE_CFG_WG_PER_CU 2  // resident bundles per CU (LDS: ~78 KB each at 4 waves)
+#endif
+constexpr int LANE_WG_PER_CU = LANE_CFG_WG_PER_CU;
 constexpr int LW = LANE_CFG_WAVES;        // waves per workgroup
 constexpr int LT = LW * LG;               // threads per workgroup
 constexpr int LKEYS = LANE_CFG_KEYS;      // LDS key capacity (global fallback beyond)

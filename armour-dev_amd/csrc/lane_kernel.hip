@@ -1,10 +1,10 @@
-// armour-mi355x — reach-set kernel, bundle form (lane_engine.h): one 512-thread workgroup per
-// bundle of 64 consecutive (world, interval) jobs, lane = job. Persistent grid over bundles; each
-// resident workgroup owns an HBM arena (union hashes, presence masks, [row][64] coefficients), a
-// header pool ([row][64]), global key buffers for operators beyond the LDS key capacity and the
-// group-value buffer between the two simplify passes. LDS (~90 KB) holds the handle table, keys,
-// group heads, staged operand hashes and the cross-wave reduction rows: one workgroup (8 waves,
-// two per SIMD) per CU.
+// armour-mi355x — reach-set kernel, bundle form (lane_engine.h): one 256-thread workgroup (4 waves)
+// per bundle of 64 consecutive (world, interval) jobs, lane = job. Persistent grid over bundles;
+// each resident workgroup owns an HBM arena (union hashes, presence masks, [row][64] coefficients),
+// a header pool ([row][64]) and global key buffers for operators beyond the LDS key capacity. LDS
+// (~78 KB) holds the handle table, keys, group heads, staged operand hashes and the cross-wave
+// reduction rows: two workgroups per CU (two waves per SIMD), so one bundle's barriers and serial
+// header work overlap the other's group rounds (measured: 8.5 % faster than one 8-wave bundle).
 #include "lane_engine.h"
 
 namespace armour {
@@ -36,7 +36,11 @@ struct LaneArgs {
     unsigned long long* prof;  // optional [2 * nops + 16] per-op cycles/terms + phase cycles
 };
 
-__global__ __attribute__((amdgpu_flat_work_group_size(LT, LT))) void lane_reach_kernel(const RobotParams* __restrict__ rpp, LaneArgs a, ReachOut out) {
+#ifndef LANE_CFG_WPE
+#define LANE_CFG_WPE 2
+#endif
+// LANE_CFG_WPE waves per SIMD (2: 256 VGPRs): e.g. one 8-wave or two 4-wave bundles per CU
+__global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_eu(LANE_CFG_WPE, LANE_CFG_WPE))) void lane_reach_kernel(const RobotParams* __restrict__ rpp, LaneArgs a, ReachOut out) {
     __shared__ LH H[MAX_SLOTS];
     __shared__ uint64_t kh[LKEYS];
     __shared__ uint32_t ki[LKEYS];

@@ -206,7 +206,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         // per-job use (~16.5k monomials) times the union inflation, with margin
         lane::LaneArgs& la = p->la;
         const long bundles = ((long)Wm * T + lane::LG - 1) / lane::LG;
-        p->lane_grid = (int)(bundles < p->ncu ? bundles : p->ncu);
+        const long slots = (long)p->ncu * lane::LANE_WG_PER_CU;
+        p->lane_grid = (int)(bundles < slots ? bundles : slots);
         const char* hc = std::getenv("ARMOUR_LANE_HCAP");
         const char* cc = std::getenv("ARMOUR_LANE_CCAP");
         la.hcap = hc ? std::atol(hc) : (1L << 16);
