@@ -84,6 +84,54 @@ __device__ inline __attribute__((always_inline)) void plane_of(const double* ga,
     for (int j = 0; j < BUF_GEN; j++) del += fabs(C0 * G[j][0] + C1 * G[j][1] + C2 * G[j][2]);
 }
 
+// Link generators 3..5 are reduce_link_PZ's radii: r_e on axis e with exact zeros elsewhere
+// (lane_engine.h emit_link). A product with one of those zeros is ±0 and adding ±0 leaves a sum
+// unchanged, so the terms below drop them: equal to the general arithmetic up to the sign of a
+// zero. E >= 0 marks a normal whose component E is zero (a plane spanned with radius E).
+template <int E>
+__device__ inline __attribute__((always_inline)) double dot_z(const double* C, const double* g) {
+    if constexpr (E == 0) return C[1] * g[1] + C[2] * g[2];
+    else if constexpr (E == 1) return C[0] * g[0] + C[2] * g[2];
+    else if constexpr (E == 2) return C[0] * g[0] + C[1] * g[1];
+    else return C[0] * g[0] + C[1] * g[1] + C[2] * g[2];
+}
+
+// mixed plane of obstacle generator ga and link generator gb = G[BUF_GEN - 6 + j] (the arithmetic
+// of plane_of): E < 0 for a box generator, E = j - 3 for radius E. del sums |A . g_k| over the 9
+// buffered generators in order; the radius terms are A_f r_f (none for f = E, where A_E = 0)
+template <int E>
+__device__ inline __attribute__((always_inline)) void mixed_plane(const double* ga, const double* gb, const double (*G)[3],
+                                                                  const double* oc, double* C, double& dd, double& del) {
+    double gc[3];
+    double nrm;
+    if constexpr (E < 0) {
+        gc[0] = ga[1] * gb[2] - ga[2] * gb[1];
+        gc[1] = ga[2] * gb[0] - ga[0] * gb[2];
+        gc[2] = ga[0] * gb[1] - ga[1] * gb[0];
+        nrm = sqrt(gc[0] * gc[0] + gc[1] * gc[1] + gc[2] * gc[2]);
+    } else {
+        const double r = gb[E];
+        if constexpr (E == 0) { gc[0] = 0.0; gc[1] = ga[2] * r; gc[2] = -(ga[1] * r); }
+        else if constexpr (E == 1) { gc[0] = -(ga[2] * r); gc[1] = 0.0; gc[2] = ga[0] * r; }
+        else { gc[0] = ga[1] * r; gc[1] = -(ga[0] * r); gc[2] = 0.0; }
+        constexpr int P = E == 0 ? 1 : 0, Q = E == 2 ? 1 : 2;
+        nrm = sqrt(gc[P] * gc[P] + gc[Q] * gc[Q]);
+    }
+    C[0] = 0; C[1] = 0; C[2] = 0;
+    if (nrm > 0) {
+#pragma unroll
+        for (int e = 0; e < 3; e++)
+            if (e != E) C[e] = gc[e] / nrm;
+    }
+    dd = dot_z<E>(C, oc);
+    del = 0.0;
+#pragma unroll
+    for (int k = 0; k < BUF_GEN - 3; k++) del += fabs(dot_z<E>(C, G[k]));
+#pragma unroll
+    for (int f = 0; f < 3; f++)
+        if (f != E) del += fabs(C[f] * G[BUF_GEN - 3 + f][f]);
+}
+
 // one monomial's contribution to a slice (k = 0) or to its derivative in x_{k-1}: the products
 // of PZsparse.cu:404-435 / 477-516 in factor order, v * 1.0 standing in for a skipped factor
 // ptab[j][g] = x_j^g (g = 0: 1.0, the skipped factor exactly), ptab[j][4 + g] = g x_j^(g-1): one
@@ -237,9 +285,13 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     __shared__ double ubuf[MAX_J * CAP_LM * 3 + NF * CAP_UM];
     auto lco = reinterpret_cast<double (*)[CAP_LM][3]>(ubuf);
     auto tco = reinterpret_cast<double (*)[CAP_UM]>(ubuf + MAX_J * CAP_LM * 3);
-    static_assert(MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5 <= MAX_J * CAP_LM * 3 + NF * CAP_UM, "plane tables");
+    constexpr int NMIX = MAX_J * MAX_OBS * OBS_GEN;
+    static_assert(MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5 + NMIX + (NMIX + 7) / 8 <= MAX_J * CAP_LM * 3 + NF * CAP_UM,
+                  "plane tables");
     auto llp = reinterpret_cast<double (*)[LL_PLANES][10]>(ubuf);
     auto oop = reinterpret_cast<double (*)[OO_PLANES][5]>(ubuf + MAX_J * LL_PLANES * 10);
+    double* mixv = ubuf + MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5;   // per (link, obstacle, i)
+    int8_t* mixc = reinterpret_cast<int8_t*>(mixv + NMIX);
     __shared__ int lcnt[MAX_J], tcnt[NF];
     __shared__ double ptab[NF][8];
     if (tid < NF) {
@@ -412,15 +464,64 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
             P[4] = del;
         }
     }
+    // the 18 mixed planes (one obstacle generator i, one link generator j) depend on both: one item
+    // per (link, obstacle, i) scans its 6 planes j = 0..5 in order and keeps the first maximum
+    // (value, and j * 2 + neg; -1: none) — 3 items per pair fill the waves that one thread per
+    // pair leaves idle
+    const int nmix = coll ? NJ * O * OBS_GEN : 0;
+    for (int u = tid; u < nmix; u += blockDim.x) {
+        const int l = u / (O * OBS_GEN), o = (u / OBS_GEN) % O, i = u % OBS_GEN;
+        const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
+        double G[BUF_GEN][3], oc[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) oc[r] = obs[o][r];
+#pragma unroll
+        for (int q = 0; q < OBS_GEN; q++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[q][r] = obs[o][(q + 1) * 3 + r];
+#pragma unroll
+        for (int q = 0; q < 6; q++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[OBS_GEN + q][r] = lgen[l][r + 3 * q];
+        double ga[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) ga[r] = obs[o][(i + 1) * 3 + r];
+        const double cc[3] = {c0, c1, c2};
+        double best = -100000000.0;
+        int code = -1;
+        auto scan = [&](auto e_tag, int j) {
+            constexpr int E = decltype(e_tag)::value;
+            double A[3], dd, del;
+            mixed_plane<E>(ga, G[OBS_GEN + j], G, oc, A, dd, del);
+            const double Ac = dot_z<E>(A, cc);
+            if (A[0] != 0 || A[1] != 0 || A[2] != 0) {
+                const double pos = Ac - (dd + del);
+                const double neg = -Ac - (-dd + del);
+                if (pos > best) { best = pos; code = 2 * j; }
+                if (neg > best) { best = neg; code = 2 * j + 1; }
+            }
+        };
+        using gen = std::integral_constant<int, -1>;
+        scan(gen{}, 0);
+        scan(gen{}, 1);
+        scan(gen{}, 2);
+        scan(std::integral_constant<int, 0>{}, 3);
+        scan(std::integral_constant<int, 1>{}, 4);
+        scan(std::integral_constant<int, 2>{}, 5);
+        mixv[u] = best;
+        mixc[u] = (int8_t)code;
+    }
     __syncthreads();
-    // one thread per (link, obstacle) scans the 36 planes in the reference's order (pairs (a, b),
-    // a < b, lexicographic: CollisionChecking.cu:26-39; pos_p before neg_p, strict >), so the first
-    // maximum wins as in the reference's serial loop
+    // one thread per (link, obstacle) completes the 36-plane scan in the reference's order (pairs
+    // (a, b), a < b, lexicographic: CollisionChecking.cu:26-39; pos_p before neg_p, strict >), so the
+    // first maximum wins as in the reference's serial loop; a mixed run (a < 3 <= b) enters as its
+    // item's first maximum, and a winning mixed plane's normal is formed again at the end
     for (int pr = tid; pr < (coll ? NJ * O : 0); pr += blockDim.x) {
         const int l = pr / O, o = pr % O;
         double best = -100000000.0;
         double B0 = 0, B1 = 0, B2 = 0;
         bool isneg = false;
+        int mwin = -1;  // winning mixed plane: i * 6 + j
         const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
         // the 9 buffered generators in registers: obstacle's 3, then the link's 6
         double G[BUF_GEN][3], oc[3];
@@ -438,14 +539,26 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         for (int a = 0; a < BUF_GEN; a++)
 #pragma unroll
             for (int b = a + 1; b < BUF_GEN; b++) {
+                if (a < OBS_GEN && b >= OBS_GEN) {
+                    if (b == OBS_GEN) {
+                        const int u = pr * OBS_GEN + a;
+                        const double v = mixv[u];
+                        const int cd = mixc[u];
+                        if (v > best) { best = v; mwin = a * 6 + (cd >> 1); isneg = cd & 1; }
+                    }
+                    continue;
+                }
                 double A0, A1, A2, dd, del, Ac;
                 if (b < OBS_GEN) {
                     const double* P = oop[o][a + b - 1];
                     A0 = P[0]; A1 = P[1]; A2 = P[2]; dd = P[3]; del = P[4];
 #pragma unroll
-                    for (int k = OBS_GEN; k < BUF_GEN; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
+                    for (int k = OBS_GEN; k < BUF_GEN - 3; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
+                    del += fabs(A0 * G[BUF_GEN - 3][0]);   // the radii (dot_z)
+                    del += fabs(A1 * G[BUF_GEN - 2][1]);
+                    del += fabs(A2 * G[BUF_GEN - 1][2]);
                     Ac = A0 * c0 + A1 * c1 + A2 * c2;
-                } else if (a >= OBS_GEN) {
+                } else {
                     const int i = a - OBS_GEN, j = b - OBS_GEN;
                     const double* P = llp[l][i * (11 - i) / 2 + j - i - 1];
                     A0 = P[0]; A1 = P[1]; A2 = P[2]; Ac = P[3];
@@ -455,19 +568,17 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
                     for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
 #pragma unroll
                     for (int k = 0; k < 6; k++) del += P[4 + k];
-                } else {
-                    plane_of(G[a], G[b], G, oc, A0, A1, A2, dd, del);
-                    Ac = A0 * c0 + A1 * c1 + A2 * c2;
                 }
                 // the reference skips a zero normal (norm > 0); for a normalised or zeroed A
                 // that is exactly "some component non-zero"
                 if (A0 != 0 || A1 != 0 || A2 != 0) {
                     const double pos = Ac - (dd + del);
                     const double neg = -Ac - (-dd + del);
-                    if (pos > best) { best = pos; B0 = A0; B1 = A1; B2 = A2; isneg = false; }
-                    if (neg > best) { best = neg; B0 = A0; B1 = A1; B2 = A2; isneg = true; }
+                    if (pos > best) { best = pos; B0 = A0; B1 = A1; B2 = A2; isneg = false; mwin = -1; }
+                    if (neg > best) { best = neg; B0 = A0; B1 = A1; B2 = A2; isneg = true; mwin = -1; }
                 }
             }
+        if (mwin >= 0) plane_normal(obs[o] + 3 * (mwin / 6 + 1), lgen[l] + 3 * (mwin % 6), B0, B1, B2);
         const long row = nt + ((long)l * d.T + t) * O + o;
         const long gi = gidx(d, slot, w, row);
         d.g[gi] = -best;
