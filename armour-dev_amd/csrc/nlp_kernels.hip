@@ -135,18 +135,17 @@ __device__ inline __attribute__((always_inline)) void mixed_plane(const double* 
 // one monomial's contribution to a slice (k = 0) or to its derivative in x_{k-1}: the products
 // of PZsparse.cu:404-435 / 477-516 in factor order, v * 1.0 standing in for a skipped factor
 // ptab[j][g] = x_j^g (g = 0: 1.0, the skipped factor exactly), ptab[j][4 + g] = g x_j^(g-1): one
-// LDS read per factor instead of a select chain (eval_kernel is VALU-issue bound)
+// LDS read per factor instead of a select chain (eval_kernel is VALU-issue bound). The reference
+// skips a term whose derivative variable has degree 0; here its factor ptab[k-1][4] = 0 makes the
+// term ±0 (coefficients and x are finite), and adding ±0 is the skip up to the sign of a zero.
 __device__ inline __attribute__((always_inline)) double slice_term(double co, int h, int k, const double (*ptab)[8]) {
     double v = co;
-    bool zero = false;
 #pragma unroll
     for (int j = 0; j < NF; j++) {
         const int g = (h >> (2 * j)) & 3;
-        const bool dj = j == k - 1;
-        zero = zero || (dj && g == 0);
-        v = v * ptab[j][g + (dj ? 4 : 0)];
+        v = v * ptab[j][g + (j == k - 1 ? 4 : 0)];
     }
-    return zero ? 0.0 : v;
+    return v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -343,10 +342,13 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     // slices (PZsparse.cu:404-435 value, :477-516 gradient): one thread per output — k = 0 the
     // value, k = 1..7 the derivative in x_{k-1} — summing its terms in monomial order. Powers come
     // from a per-variable table (ptab, filled with the staging), the very products ipow forms.
+    // The NF * 8 torque outputs (the longest sums) fill wave 0 alone, the link outputs start at
+    // thread 64: no wave runs both loops.
     const int nlk = NJ * 3 * 8;
-    for (int u = tid; u < ((d.diag & 1) ? 0 : nlk + NF * 8); u += blockDim.x) {
-      if (u < nlk) {
-        const int l = u / 24, e = (u / 8) % 3, k = u % 8;
+    for (int u = tid; u < ((d.diag & 1) ? 0 : 64 + nlk); u += blockDim.x) {
+      if (u >= 64) {
+        const int ul = u - 64;
+        const int l = ul / 24, e = (ul / 8) % 3, k = ul % 8;
         const long base = jt * NJ + l;
         double c = k == 0 ? d.ro.link_center[base * 3 + e] : 0.0;
         const int cnt = lcnt[l];
@@ -364,7 +366,8 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         }
       } else {
         // torque rows (NLPclass.cu:304-309, 376-380)
-        const int j = (u - nlk) / 8, k = (u - nlk) % 8;
+        if (u >= NF * 8) continue;
+        const int j = u / 8, k = u % 8;
         const long base = jt * NF + j;
         double c = k == 0 ? d.ro.tq_center[base] : 0.0;
         const int cnt = tcnt[j];
