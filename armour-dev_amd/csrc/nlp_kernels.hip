@@ -26,17 +26,36 @@ __device__ inline double wave_min(double v) {
     for (int m = 1; m < 64; m <<= 1) v = fmin(v, xor_f64(v, m));
     return v;
 }
-// kind: 0 sum, 1 max, 2 min; result written by thread 0 to out
-__device__ inline void block_reduce(double v, int kind, double* lds, double* out) {
-    v = kind == 0 ? wave_sum(v) : kind == 1 ? wave_max(v) : wave_min(v);
+// N values at once, the arithmetic of N block_reduce calls (wave reduction, then the waves in
+// order) with one barrier: the N wave reductions are independent and interleave. kinds[i]: 0 sum,
+// 1 max, 2 min. out[i] written by thread i; lds holds (blockDim / 64) * N doubles.
+template <int N>
+__device__ inline void block_reduce_n(double (&v)[N], const int (&kinds)[N], double* lds, double* out) {
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // groups of 8 interleave; a scheduling barrier between groups bounds the live registers
+#pragma unroll
+    for (int g = 0; g < N; g += 8) {
+#pragma unroll
+        for (int i = g; i < (g + 8 < N ? g + 8 : N); i++)
+            v[i] = kinds[i] == 0 ? wave_sum(v[i]) : kinds[i] == 1 ? wave_max(v[i]) : wave_min(v[i]);
+        if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+            for (int i = g; i < (g + 8 < N ? g + 8 : N); i++) lds[wave * N + i] = v[i];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) lds[wave] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double s = lds[0];
-        for (int i = 1; i < nw; i++) s = kind == 0 ? s + lds[i] : kind == 1 ? fmax(s, lds[i]) : fmin(s, lds[i]);
-        *out = s;
+    const int i = threadIdx.x;
+    if (i < N) {
+        int kind = 0;
+#pragma unroll
+        for (int q = 0; q < N; q++) if (q == i) kind = kinds[q];
+        double s = lds[i];
+        for (int k = 1; k < nw; k++) {
+            const double t = lds[k * N + i];
+            s = kind == 0 ? s + t : kind == 1 ? fmax(s, t) : fmin(s, t);
+        }
+        out[i] = s;
     }
 }
 
@@ -652,7 +671,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
     const int w = blockIdx.y;
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    __shared__ double lds[ROW_THREADS / 64];
+    __shared__ double lds[(ROW_THREADS / 64) * 53];
     double rdp[NF], M[28], u1[NF], u2[NF];
     double inf_p = 0, compl0 = 0, cm = 0, sumz = 0;
 #pragma unroll
@@ -706,18 +725,16 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
         }
     }
     double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
+    double v[53];
+    int kinds[53];
 #pragma unroll
-    for (int j = 0; j < NF; j++) block_reduce(rdp[j], 0, lds, &out[j]);
-    block_reduce(inf_p, 1, lds, &out[7]);
-    block_reduce(compl0, 1, lds, &out[8]);
-    block_reduce(cm, 1, lds, &out[9]);
-    block_reduce(sumz, 0, lds, &out[10]);
+    for (int j = 0; j < NF; j++) { v[j] = rdp[j]; v[39 + j] = u1[j]; v[46 + j] = u2[j]; }
+    v[7] = inf_p; v[8] = compl0; v[9] = cm; v[10] = sumz;
 #pragma unroll
-    for (int k = 0; k < 28; k++) block_reduce(M[k], 0, lds, &out[11 + k]);
+    for (int k = 0; k < 28; k++) v[11 + k] = M[k];
 #pragma unroll
-    for (int j = 0; j < NF; j++) block_reduce(u1[j], 0, lds, &out[39 + j]);
-#pragma unroll
-    for (int j = 0; j < NF; j++) block_reduce(u2[j], 0, lds, &out[46 + j]);
+    for (int k = 0; k < 53; k++) kinds[k] = (k >= 7 && k <= 9) ? 1 : 0;
+    block_reduce_n(v, kinds, lds, out);
 }
 
 __device__ bool chol_solve7(const double* M, double shift, const double* b, double* x) {
@@ -801,7 +818,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
     const int w = blockIdx.y;
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    __shared__ double lds[ROW_THREADS / 64];
+    __shared__ double lds[(ROW_THREADS / 64) * 53];
     const double mu = S.mu;
     const double tau = fmax(d.opt.tau_min, 1.0 - mu);
     double ap = 1.0, ad = 1.0, rp1 = 0, bdir = 0, logs = 0, wa[NF], wb[NF];
@@ -841,15 +858,14 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
         for (int j = 0; j < NF; j++) { wa[j] += za * a[j]; wb[j] += zb * a[j]; }
     }
     double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
-    block_reduce(ap, 2, lds, &out[0]);
-    block_reduce(ad, 2, lds, &out[1]);
-    block_reduce(rp1, 0, lds, &out[2]);
-    block_reduce(bdir, 0, lds, &out[3]);
-    block_reduce(logs, 0, lds, &out[4]);
+    double v[19];
+    int kinds[19];
+    v[0] = ap; v[1] = ad; v[2] = rp1; v[3] = bdir; v[4] = logs;
 #pragma unroll
-    for (int j = 0; j < NF; j++) block_reduce(wa[j], 0, lds, &out[5 + j]);
+    for (int j = 0; j < NF; j++) { v[5 + j] = wa[j]; v[12 + j] = wb[j]; }
 #pragma unroll
-    for (int j = 0; j < NF; j++) block_reduce(wb[j], 0, lds, &out[12 + j]);
+    for (int k = 0; k < 19; k++) kinds[k] = k < 2 ? 2 : 0;
+    block_reduce_n(v, kinds, lds, out);
 }
 
 __global__ void ipm_world_B(NlpDev d) {
@@ -891,7 +907,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
     const int w = blockIdx.y;
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
-    __shared__ double lds[ROW_THREADS / 64];
+    __shared__ double lds[(ROW_THREADS / 64) * 53];
     double logt = 0, rpt = 0;
     const long r0 = (long)blockIdx.x * d.chunk;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
@@ -903,8 +919,9 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
         if (has_hi(d, U)) { const double st = d.shi[i] + S.alpha * d.dshi[i]; logt += log(st); rpt += fabs((U - v) - st); }
     }
     double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
-    block_reduce(logt, 0, lds, &out[0]);
-    block_reduce(rpt, 0, lds, &out[1]);
+    double v[2] = {logt, rpt};
+    const int kinds[2] = {0, 0};
+    block_reduce_n(v, kinds, lds, out);
 }
 
 __global__ void ipm_world_C(NlpDev d) {
@@ -961,7 +978,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
     const int w = blockIdx.y;
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    __shared__ double lds[ROW_THREADS / 64];
+    __shared__ double lds[(ROW_THREADS / 64) * 53];
     const double mu = S.mu, ad = S.ad, alpha = S.alpha, ks = d.opt.kappa_sigma;
     double wn[NF];
 #pragma unroll
@@ -991,8 +1008,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
         for (int j = 0; j < NF; j++) wn[j] += wv * a[j];
     }
     double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
-#pragma unroll
-    for (int j = 0; j < NF; j++) block_reduce(wn[j], 0, lds, &out[j]);
+    const int kinds[NF] = {};
+    block_reduce_n(wn, kinds, lds, out);
 }
 
 __global__ void ipm_world_D(NlpDev d) {
