@@ -764,21 +764,48 @@ __device__ bool chol_solve7(const double* M, double shift, const double* b, doub
     return true;
 }
 
-__global__ void ipm_world_A(NlpDev d, int nside) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= d.W) return;
-    WorldState& S = d.ws[w];
-    if (S.status != 0) return;
-    if (S.iter >= d.opt.max_iter) { S.status = 2; return; }  // oracle: loop ends without a final check
-    double P[KA];
-    for (int k = 0; k < 53; k++) P[k] = 0;
-    for (int b = 0; b < d.nblk; b++) {
-        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
-        for (int k = 0; k < 53; k++) {
-            if (k >= 7 && k <= 9) P[k] = fmax(P[k], in[k]);
-            else P[k] = P[k] + in[k];
+// world w's row-block partials [0, N) combined over the blocks in block order, one lane per value
+// (the arithmetic of a serial loop over the blocks), returned wave-uniform. op: 0 sum, 1 max, 2 min
+// onto init. The per-world kernels run one wave per world: the nblk dependent load rounds of a
+// single thread become one round per lane.
+template <int N>
+__device__ inline void world_partials(const NlpDev& d, int w, const double (&init)[N], const int (&op)[N], double (&P)[N]) {
+    const int lane = threadIdx.x & 63;
+    double s = 0;
+    int o = 0;
+#pragma unroll
+    for (int q = 0; q < N; q++)
+        if (q == lane) { s = init[q]; o = op[q]; }
+    if (lane < N) {
+        const double* in = d.partial + (long)w * d.nblk * KA + lane;
+        for (int b = 0; b < d.nblk; b++) {
+            const double x = in[(long)b * KA];
+            s = o == 0 ? s + x : o == 1 ? fmax(s, x) : fmin(s, x);
         }
     }
+    const uint64_t u = __builtin_bit_cast(uint64_t, s);
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, q);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), q);
+        P[q] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    }
+}
+
+__global__ void ipm_world_A(NlpDev d, int nside) {
+    const int w = blockIdx.x;
+    WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    if (S.iter >= d.opt.max_iter) {  // oracle: loop ends without a final check
+        if (threadIdx.x == 0) S.status = 2;
+        return;
+    }
+    double P[53], init[53];
+    int op[53];
+#pragma unroll
+    for (int k = 0; k < 53; k++) { init[k] = 0; op[k] = (k >= 7 && k <= 9) ? 1 : 0; }
+    world_partials(d, w, init, op, P);
+    if (threadIdx.x != 0) return;
     const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
     double rd[NF], inf_d = 0;
     for (int j = 0; j < NF; j++) { rd[j] = grad[j] - P[j]; inf_d = fmax(inf_d, fabs(rd[j])); }
@@ -869,19 +896,15 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
 }
 
 __global__ void ipm_world_B(NlpDev d) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= d.W) return;
+    const int w = blockIdx.x;
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    double P[19];
-    P[0] = 1.0; P[1] = 1.0;
-    for (int k = 2; k < 19; k++) P[k] = 0;
-    for (int b = 0; b < d.nblk; b++) {
-        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
-        P[0] = fmin(P[0], in[0]);
-        P[1] = fmin(P[1], in[1]);
-        for (int k = 2; k < 19; k++) P[k] = P[k] + in[k];
-    }
+    double P[19], init[19];
+    int op[19];
+#pragma unroll
+    for (int k = 0; k < 19; k++) { init[k] = k < 2 ? 1.0 : 0.0; op[k] = k < 2 ? 2 : 0; }
+    world_partials(d, w, init, op, P);
+    if (threadIdx.x != 0) return;
     const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
     const double f = d.f[S.cur * d.W + w];
     double gdx = 0;
@@ -925,16 +948,15 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
 }
 
 __global__ void ipm_world_C(NlpDev d) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= d.W) return;
+    const int w = blockIdx.x;
     WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
-    double logt = 0, rpt = 0;
-    for (int b = 0; b < d.nblk; b++) {
-        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
-        logt = logt + in[0];
-        rpt = rpt + in[1];
-    }
+    double P[2];
+    const double init[2] = {0.0, 0.0};
+    const int op[2] = {0, 0};
+    world_partials(d, w, init, op, P);
+    if (threadIdx.x != 0) return;
+    const double logt = P[0], rpt = P[1];
     S.nevals++;
     const double ft = d.f[(1 - S.cur) * d.W + w];
     const double phit = ft - S.mu * logt, thetat = rpt;
@@ -1013,16 +1035,14 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
 }
 
 __global__ void ipm_world_D(NlpDev d) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= d.W) return;
+    const int w = blockIdx.x;
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
     double wn[NF];
-    for (int j = 0; j < NF; j++) wn[j] = 0;
-    for (int b = 0; b < d.nblk; b++) {
-        const double* in = d.partial + ((long)w * d.nblk + b) * KA;
-        for (int j = 0; j < NF; j++) wn[j] = wn[j] + in[j];
-    }
+    const double init[NF] = {};
+    const int op[NF] = {};
+    world_partials(d, w, init, op, wn);
+    if (threadIdx.x != 0) return;
     const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
     const double* gradt = d.grad + ((long)(1 - S.cur) * d.W + w) * NF;
     double sv[NF], y[NF], Hs[NF], ss = 0, sy = 0;

@@ -383,21 +383,21 @@ static int run_solver(armour_planner* p) {
     const int ns = nside_count(p);
     for (int it = 0; it <= d.opt.max_iter; it++) {
         hipLaunchKernelGGL(ipm_rows_A, rows, dim3(ROW_THREADS), 0, p->stream, d);
-        hipLaunchKernelGGL(ipm_world_A, dim3(wb), dim3(64), 0, p->stream, d, ns);
+        hipLaunchKernelGGL(ipm_world_A, dim3(W), dim3(64), 0, p->stream, d, ns);
         hipLaunchKernelGGL(ipm_rows_B, rows, dim3(ROW_THREADS), 0, p->stream, d);
-        hipLaunchKernelGGL(ipm_world_B, dim3(wb), dim3(64), 0, p->stream, d);
+        hipLaunchKernelGGL(ipm_world_B, dim3(W), dim3(64), 0, p->stream, d);
         for (int ls = 0; ls < d.opt.max_ls; ls++) {
             HIPCK(hipMemsetAsync(d.flags, 0, sizeof(int), p->stream));
             hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 1);
             hipLaunchKernelGGL(ipm_rows_C, rows, dim3(ROW_THREADS), 0, p->stream, d);
-            hipLaunchKernelGGL(ipm_world_C, dim3(wb), dim3(64), 0, p->stream, d);
+            hipLaunchKernelGGL(ipm_world_C, dim3(W), dim3(64), 0, p->stream, d);
             HIPCK(hipMemcpyAsync(p->h_flags, d.flags, sizeof(int), hipMemcpyDeviceToHost, p->stream));
             HIPCK(hipStreamSynchronize(p->stream));
             if (p->h_flags[0] == 0) break;
         }
         HIPCK(hipMemsetAsync(d.flags + 1, 0, sizeof(int), p->stream));
         hipLaunchKernelGGL(ipm_rows_D, rows, dim3(ROW_THREADS), 0, p->stream, d);
-        hipLaunchKernelGGL(ipm_world_D, dim3(wb), dim3(64), 0, p->stream, d);
+        hipLaunchKernelGGL(ipm_world_D, dim3(W), dim3(64), 0, p->stream, d);
         HIPCK(hipGetLastError());
         HIPCK(hipMemcpyAsync(p->h_flags + 1, d.flags + 1, sizeof(int), hipMemcpyDeviceToHost, p->stream));
         HIPCK(hipStreamSynchronize(p->stream));
