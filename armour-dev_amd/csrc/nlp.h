@@ -61,7 +61,9 @@ struct NlpDev {
     double* J;
     double* f;
     double* grad;
-    double* link_c;         // [W][T][NJ][3] sliced link centres of the latest evaluation
+    double* link_c;         // [3][lcs]: [slot][W][T][NJ][3] sliced link centres of each eval slot's
+                            // latest evaluation; region 2 the final iterate's (feasible_kernel)
+    long lcs;
     // solver row state [W][R]
     double *slo, *shi, *zlo, *zhi, *dslo, *dshi, *dzlo, *dzhi, *rplo, *rphi;
     double* partial;        // [W][nblk][KA]

@@ -279,8 +279,8 @@ __device__ double wrap_to_pi(double a) {
 // ------------------------------------------------------------------------------------------
 // g(x) and dense Jacobian, grid (T, W). mode 0: ws.x into slot 0 (start point,
 // armour_eval_constraints); mode 1: the line-search trial ws.xt into the non-current slot (worlds
-// still searching only); mode 2: ws.x into the non-current slot, so the link centres hold the
-// final iterate's values
+// still searching only). The sliced link centres go to the slot's own region (feasible_kernel
+// copies the current slot's, the final iterate's, out).
 __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) {
     const int t = blockIdx.x, w = blockIdx.y;
     WorldState& S = d.ws[w];
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
             const double r = d.ro.link_rad[base * 3 + e];
             const double cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
             lc[l][e] = cc;
-            d.link_c[base * 3 + e] = cc;
+            d.link_c[slot * d.lcs + base * 3 + e] = cc;
         } else {
             dlc[l][k - 1][e] = c;
         }
@@ -1100,6 +1100,10 @@ __global__ void feasible_kernel(NlpDev d, int* feasible) {
         else b = v < d.L[i] || v > d.U[i];
         if (b) atomicOr(&bad, 1);
     }
+    const long n = (long)d.T * d.NJ * 3;
+    const double* src = d.link_c + S.cur * d.lcs + w * n;
+    double* dst = d.link_c + 2 * d.lcs + w * n;
+    for (long i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
     __syncthreads();
     if (threadIdx.x == 0) feasible[w] = bad ? 0 : 1;
 }

@@ -251,11 +251,12 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     d.NJ = NJ;
     d.ro = ro;
     if (cfg->max_iter > 0) d.opt.max_iter = cfg->max_iter;
+    d.lcs = (long)(jobs * NJ * 3);
     const size_t mmax = (size_t)NF * T + (size_t)T * NJ * Om + NF * 4;
     const size_t Rmax = mmax + NF;
     if ((rc = p->alloc(&d.L, Wm * Rmax)) || (rc = p->alloc(&d.U, Wm * Rmax)) || (rc = p->alloc(&d.g, 2 * Wm * mmax)) ||
         (rc = p->alloc(&d.J, 2 * Wm * mmax * NF)) || (rc = p->alloc(&d.f, 2 * (size_t)Wm)) ||
-        (rc = p->alloc(&d.grad, 2 * (size_t)Wm * NF)) || (rc = p->alloc(&d.link_c, jobs * NJ * 3)))
+        (rc = p->alloc(&d.grad, 2 * (size_t)Wm * NF)) || (rc = p->alloc(&d.link_c, 3 * jobs * NJ * 3)))
         return rc;
     double** rowbufs[] = {&d.slo, &d.shi, &d.zlo, &d.zhi, &d.dslo, &d.dshi, &d.dzlo, &d.dzhi, &d.rplo, &d.rphi};
     for (double** b : rowbufs)
@@ -403,8 +404,8 @@ static int run_solver(armour_planner* p) {
         HIPCK(hipStreamSynchronize(p->stream));
         if (p->h_flags[1] == 0) break;  // every world converged, hit the cap or failed
     }
-    // sliced link centres at the final iterate (armour_joint_position_center.out payload)
-    hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 2);
+    // feasibility re-check and the sliced link centres at the final iterate (the current slot's,
+    // armour_joint_position_center.out payload)
     hipLaunchKernelGGL(feasible_kernel, dim3(W), dim3(256), 0, p->stream, d, p->feas);
     HIPCK(hipGetLastError());
     return 0;
@@ -572,7 +573,7 @@ int armour_get_link_centers(armour_planner* p, int w, double* c) {
     if (!p || !c) return fail(ARMOUR_E_ARG, "null argument");
     if (!p->planned) return fail(ARMOUR_E_STATE, "no plan");
     if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
-    HIPCK(hipMemcpy(c, p->d.link_c + (size_t)w * p->T * p->NJ * 3, sizeof(double) * p->T * p->NJ * 3, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(c, p->d.link_c + 2 * p->d.lcs + (size_t)w * p->T * p->NJ * 3, sizeof(double) * p->T * p->NJ * 3, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -1,4 +1,5 @@
-"""Bitwise A/B of whole plans (k_opt, status, iterations, evaluations, cost, KKT error) between two
+"""Bitwise A/B of whole plans (k_opt, status, iterations, evaluations, cost, KKT error, final link
+centres) between two
 library builds, at the bench configuration (development tool).
 usage: python tools/plan_ab.py <lib_a> <lib_b> [worlds]"""
 import os, subprocess, sys
@@ -13,7 +14,8 @@ W = int(sys.argv[2])
 P = A.Planner(T=100, max_obstacles=20, max_worlds=W)
 res, _ = P.plan([A.make_world(1000 + s, 20) for s in range(W)])
 np.save(sys.argv[1], np.array([np.concatenate([r["k_opt"], [r["feasible"], r["status"], r["iterations"],
-                                               r["evaluations"], r["cost"], r["kkt"]]]) for r in res]))
+                                               r["evaluations"], r["cost"], r["kkt"]], P.link_centers(w).ravel()])
+                               for w, r in enumerate(res)]))
 '''
 W = sys.argv[3] if len(sys.argv) > 3 else "64"
 outs = []
