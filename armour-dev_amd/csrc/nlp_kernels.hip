@@ -992,7 +992,7 @@ __global__ void ipm_world_C(NlpDev d) {
     }
     S.alpha *= 0.5;
     for (int j = 0; j < NF; j++) S.xt[j] = S.x[j] + S.alpha * S.dx[j];
-    atomicOr(&d.flags[0], 1);
+    d.flags[0] = 1;  // mapped host memory: a plain store, every writer stores 1
 }
 
 // pass D: accept the trial point — slacks, multipliers, BFGS ingredients
@@ -1079,7 +1079,7 @@ __global__ void ipm_world_D(NlpDev d) {
     S.nfail = S.accepted_ok ? 0 : S.nfail + 1;
     S.iter++;
     if (S.nfail >= 3) S.status = 3;
-    if (S.status == 0) atomicOr(&d.flags[1], 1);
+    if (S.status == 0) d.flags[1] = 1;
 }
 
 // finalize_solution's feasibility re-check (NLPclass.cu:449-538): one block per world

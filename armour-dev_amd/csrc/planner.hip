@@ -263,9 +263,12 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         if ((rc = p->alloc(b, Wm * Rmax))) return rc;
     const int nblk_max = (int)((Rmax + 2047) / 2048);
     if ((rc = p->alloc(&d.partial, (size_t)Wm * nblk_max * KA)) || (rc = p->alloc(&d.ws, (size_t)Wm)) ||
-        (rc = p->alloc(&d.flags, 4)) || (rc = p->alloc(&p->feas, (size_t)Wm)))
+        (rc = p->alloc(&p->feas, (size_t)Wm)))
         return rc;
-    HIPCK(hipHostMalloc((void**)&p->h_flags, 4 * sizeof(int)));
+    // the solver's two continue flags live in mapped host memory: kernels store 1 into them, the
+    // host clears and reads them between synchronised rounds (no fill or copy per round)
+    HIPCK(hipHostMalloc((void**)&p->h_flags, 4 * sizeof(int), hipHostMallocMapped));
+    HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
     HIPCK(hipHostMalloc((void**)&p->h_ws, Wm * sizeof(WorldState)));
     HIPCK(hipHostMalloc((void**)&p->h_f, 2 * Wm * sizeof(double)));
     HIPCK(hipHostMalloc((void**)&p->h_feas, Wm * sizeof(int)));
@@ -388,21 +391,19 @@ static int run_solver(armour_planner* p) {
         hipLaunchKernelGGL(ipm_rows_B, rows, dim3(ROW_THREADS), 0, p->stream, d);
         hipLaunchKernelGGL(ipm_world_B, dim3(W), dim3(64), 0, p->stream, d);
         for (int ls = 0; ls < d.opt.max_ls; ls++) {
-            HIPCK(hipMemsetAsync(d.flags, 0, sizeof(int), p->stream));
+            p->h_flags[0] = 0;  // no kernel in flight writes it (world_C's last round was synchronised)
             hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 1);
             hipLaunchKernelGGL(ipm_rows_C, rows, dim3(ROW_THREADS), 0, p->stream, d);
             hipLaunchKernelGGL(ipm_world_C, dim3(W), dim3(64), 0, p->stream, d);
-            HIPCK(hipMemcpyAsync(p->h_flags, d.flags, sizeof(int), hipMemcpyDeviceToHost, p->stream));
             HIPCK(hipStreamSynchronize(p->stream));
-            if (p->h_flags[0] == 0) break;
+            if (((volatile int*)p->h_flags)[0] == 0) break;
         }
-        HIPCK(hipMemsetAsync(d.flags + 1, 0, sizeof(int), p->stream));
+        p->h_flags[1] = 0;
         hipLaunchKernelGGL(ipm_rows_D, rows, dim3(ROW_THREADS), 0, p->stream, d);
         hipLaunchKernelGGL(ipm_world_D, dim3(W), dim3(64), 0, p->stream, d);
         HIPCK(hipGetLastError());
-        HIPCK(hipMemcpyAsync(p->h_flags + 1, d.flags + 1, sizeof(int), hipMemcpyDeviceToHost, p->stream));
         HIPCK(hipStreamSynchronize(p->stream));
-        if (p->h_flags[1] == 0) break;  // every world converged, hit the cap or failed
+        if (((volatile int*)p->h_flags)[1] == 0) break;  // every world converged, hit the cap or failed
     }
     // feasibility re-check and the sliced link centres at the final iterate (the current slot's,
     // armour_joint_position_center.out payload)
