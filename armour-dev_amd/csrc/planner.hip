@@ -385,7 +385,11 @@ static int run_solver(armour_planner* p) {
     hipLaunchKernelGGL(ipm_rows_init, rows, dim3(ROW_THREADS), 0, p->stream, d);
     HIPCK(hipGetLastError());
     const int ns = nside_count(p);
-    for (int it = 0; it <= d.opt.max_iter; it++) {
+    // One host synchronisation per line-search round. world_D's "any world running" flag is read
+    // at the next iteration's first round: the kernels queued in between exit at once for worlds
+    // that are no longer running, so a finished batch only costs one round of empty launches.
+    bool done = false;
+    for (int it = 0; it <= d.opt.max_iter && !done; it++) {
         hipLaunchKernelGGL(ipm_rows_A, rows, dim3(ROW_THREADS), 0, p->stream, d);
         hipLaunchKernelGGL(ipm_world_A, dim3(W), dim3(64), 0, p->stream, d, ns);
         hipLaunchKernelGGL(ipm_rows_B, rows, dim3(ROW_THREADS), 0, p->stream, d);
@@ -396,14 +400,17 @@ static int run_solver(armour_planner* p) {
             hipLaunchKernelGGL(ipm_rows_C, rows, dim3(ROW_THREADS), 0, p->stream, d);
             hipLaunchKernelGGL(ipm_world_C, dim3(W), dim3(64), 0, p->stream, d);
             HIPCK(hipStreamSynchronize(p->stream));
+            if (ls == 0 && it > 0 && ((volatile int*)p->h_flags)[1] == 0) {
+                done = true;  // every world converged, hit the cap or failed at the previous iteration
+                break;
+            }
             if (((volatile int*)p->h_flags)[0] == 0) break;
         }
-        p->h_flags[1] = 0;
+        if (done) break;
+        p->h_flags[1] = 0;  // the previous world_D completed before the synchronisation above
         hipLaunchKernelGGL(ipm_rows_D, rows, dim3(ROW_THREADS), 0, p->stream, d);
         hipLaunchKernelGGL(ipm_world_D, dim3(W), dim3(64), 0, p->stream, d);
         HIPCK(hipGetLastError());
-        HIPCK(hipStreamSynchronize(p->stream));
-        if (((volatile int*)p->h_flags)[1] == 0) break;  // every world converged, hit the cap or failed
     }
     // feasibility re-check and the sliced link centres at the final iterate (the current slot's,
     // armour_joint_position_center.out payload)
