@@ -90,6 +90,16 @@ struct armour_planner {
     }
 };
 
+// rows per block of the IPM row passes (ARMOUR_ROW_CHUNK overrides for diagnostics, a multiple of
+// 256). Measured at 327 worlds (tools/chunk_sweep.sh): 2048 rows 34.8 ms of NLP, 1024 34.2 ms, 512
+// 36.5 ms, 256 43.1 ms: shorter per-thread row loops help the latency-bound tail iterations until
+// the per-block reductions dominate.
+static int row_chunk() {
+    const char* e = std::getenv("ARMOUR_ROW_CHUNK");
+    const int c = e ? std::atoi(e) : 1024;
+    return (c >= 256 && c % 256 == 0) ? c : 1024;
+}
+
 static int planner_init(armour_planner* p, const armour_config* cfg, const armour_robot* robot) {
     p->cfg = *cfg;
     if (!robot && cfg->robot != 0) return fail(ARMOUR_E_ARG, "unknown robot id");
@@ -261,7 +271,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     double** rowbufs[] = {&d.slo, &d.shi, &d.zlo, &d.zhi, &d.dslo, &d.dshi, &d.dzlo, &d.dzhi, &d.rplo, &d.rphi};
     for (double** b : rowbufs)
         if ((rc = p->alloc(b, Wm * Rmax))) return rc;
-    const int nblk_max = (int)((Rmax + 2047) / 2048);
+    const int nblk_max = (int)((Rmax + row_chunk() - 1) / row_chunk());
     if ((rc = p->alloc(&d.partial, (size_t)Wm * nblk_max * KA)) || (rc = p->alloc(&d.ws, (size_t)Wm)) ||
         (rc = p->alloc(&p->feas, (size_t)Wm)))
         return rc;
@@ -310,7 +320,7 @@ static int upload_worlds(armour_planner* p, int W, const armour_world* worlds) {
     d.O = O;
     d.m = NF * p->T + p->T * p->NJ * O + NF * 4;
     d.R = d.m + NF;
-    d.chunk = 2048;
+    d.chunk = row_chunk();
     d.nblk = (d.R + d.chunk - 1) / d.chunk;
     return 0;
 }
