@@ -35,6 +35,13 @@ class World(ctypes.Structure):
                 ("q_des", ctypes.c_double * NF), ("num_obstacles", ctypes.c_int), ("obstacles", _dp)]
 
 
+_WORLD_DTYPE = np.dtype({"names": ["q0", "qd0", "qdd0", "q_des", "num_obstacles", "obstacles"],
+                         "formats": [(np.float64, NF)] * 4 + [np.int32, np.uintp],
+                         "offsets": [World.q0.offset, World.qd0.offset, World.qdd0.offset, World.q_des.offset,
+                                     World.num_obstacles.offset, World.obstacles.offset],
+                         "itemsize": ctypes.sizeof(World)})
+
+
 class Result(ctypes.Structure):
     _fields_ = [("k_opt", ctypes.c_double * NF), ("feasible", ctypes.c_int), ("solver_status", ctypes.c_int),
                 ("iterations", ctypes.c_int), ("evaluations", ctypes.c_int), ("cost", ctypes.c_double),
@@ -137,17 +144,21 @@ class Planner:
         return lib().armour_num_constraints(self.h, O)
 
     def _worlds(self, worlds):
-        arr = (World * len(worlds))()
-        self._keep = []
-        for i, (q0, qd0, qdd0, qdes, obs) in enumerate(worlds):
-            w = arr[i]
-            for j in range(NF):
-                w.q0[j], w.qd0[j], w.qdd0[j], w.q_des[j] = q0[j], qd0[j], qdd0[j], qdes[j]
-            o = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, 12))
-            self._keep.append(o)
-            w.num_obstacles = o.shape[0]
-            w.obstacles = _ptr(o) if o.shape[0] else None
-        self.O = arr[0].num_obstacles
+        # the armour_world array filled through a NumPy view of its fields (one vectorised store
+        # per field instead of a ctypes assignment per element); obstacles in one contiguous block
+        n = len(worlds)
+        arr = (World * n)()
+        view = np.frombuffer(arr, dtype=_WORLD_DTYPE)
+        for k, f in enumerate(("q0", "qd0", "qdd0", "q_des")):
+            view[f] = np.asarray([w[k] for w in worlds], dtype=np.float64).reshape(n, NF)
+        obs = [np.asarray(w[4], dtype=np.float64).reshape(-1, 12) for w in worlds]
+        counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
+        block = np.ascontiguousarray(np.concatenate(obs) if counts.sum() else np.zeros((0, 12)))
+        self._keep = [block]
+        view["num_obstacles"] = counts
+        starts = np.concatenate([[0], np.cumsum(counts)[:-1]]) * 12 * 8
+        view["obstacles"] = np.where(counts > 0, block.ctypes.data + starts, 0)
+        self.O = int(counts[0]) if n else 0
         return arr
 
     def plan(self, worlds):
