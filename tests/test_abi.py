@@ -5,6 +5,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 import armour_amd as A
@@ -86,3 +87,25 @@ def test_bad_config_rejected_before_device():
     """Argument checks come first (KPR/Parameters.h: NUM_TIME_STEPS must be even)."""
     with pytest.raises(A.ArmourError, match="even"):
         A.Planner(T=11, max_obstacles=2, max_worlds=1)
+
+
+def test_world_batch_marshalling():
+    # Planner._worlds fills the armour_world array (include/armour_hip.h) through a NumPy view:
+    # every field must equal the inputs, obstacle pointers must address each world's own block,
+    # and a world without obstacles gets a null pointer
+    import ctypes
+    import types
+    worlds = [A.make_world(s, 20) for s in range(5)] + [A.make_world(9, 0), A.make_world(11, 3)]
+    arr = A.Planner._worlds(types.SimpleNamespace(), worlds)
+    assert ctypes.sizeof(arr) == len(worlds) * ctypes.sizeof(A.World)
+    for i, w in enumerate(worlds):
+        a = arr[i]
+        for k, f in enumerate(("q0", "qd0", "qdd0", "q_des")):
+            assert np.array_equal(np.array(getattr(a, f)[:]), np.asarray(w[k], dtype=float)), (i, f)
+        o = np.asarray(w[4], dtype=float).reshape(-1, 12)
+        assert a.num_obstacles == o.shape[0]
+        if o.shape[0]:
+            got = np.ctypeslib.as_array(a.obstacles, shape=(o.shape[0] * 12,)).reshape(-1, 12)
+            assert np.array_equal(got, o), i
+        else:
+            assert not a.obstacles
