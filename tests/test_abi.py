@@ -96,7 +96,8 @@ def test_world_batch_marshalling():
     import ctypes
     import types
     worlds = [A.make_world(s, 20) for s in range(5)] + [A.make_world(9, 0), A.make_world(11, 3)]
-    arr = A.Planner._worlds(types.SimpleNamespace(), worlds)
+    holder = types.SimpleNamespace()   # owns the obstacle block, as a Planner does (self._keep)
+    arr = A.Planner._worlds(holder, worlds)
     assert ctypes.sizeof(arr) == len(worlds) * ctypes.sizeof(A.World)
     for i, w in enumerate(worlds):
         a = arr[i]
