@@ -3,9 +3,10 @@
 //   eval_kernel         g(x) and its dense Jacobian (KPR/NLPclass.cu:207-396): PZ slicing
 //                       (PZsparse.cu:404-555), collision rows (CollisionChecking.cu:230-299) with
 //                       the buffered-obstacle hyperplanes (:136-228) computed in place and a
-//                       wave-wide argmax in the reference's scan order, torque and extremum rows
+//                       per-(link, obstacle) scan in the reference's plane order, torque and
+//                       extremum rows
 //   ipm_*               armour-IPM (oracle/src/ipm.cpp), one row-parallel pass per phase with
-//                       deterministic block partials and one thread per world for the 7x7 algebra
+//                       deterministic block partials and one wave per world for the 7x7 algebra
 //   feasible_kernel     finalize_solution's re-check (KPR/NLPclass.cu:449-538)
 #include "nlp.h"
 
@@ -13,8 +14,6 @@ namespace armour {
 
 // ------------------------------------------------------------------------------------------
 // helpers
-__device__ inline double ipow(double x, int d) { return d == 0 ? 1.0 : d == 1 ? x : d == 2 ? x * x : x * x * x; }
-
 // wave_sum (wave.h): DPP / permlane butterfly
 __device__ inline double wave_max(double v) {
 #pragma unroll
@@ -87,22 +86,6 @@ __device__ inline __attribute__((always_inline)) void plane_normal(const double*
     if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
 }
 
-// plane of the generator pair (ga, gb) (the arithmetic of buffered_plane below, pair given)
-__device__ inline __attribute__((always_inline)) void plane_of(const double* ga, const double* gb, const double (*G)[3],
-                                                               const double* oc, double& C0, double& C1, double& C2,
-                                                               double& dd, double& del) {
-    const double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
-    const double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
-    const double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
-    const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
-    C0 = 0; C1 = 0; C2 = 0;
-    if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
-    dd = C0 * oc[0] + C1 * oc[1] + C2 * oc[2];
-    del = 0.0;
-#pragma unroll
-    for (int j = 0; j < BUF_GEN; j++) del += fabs(C0 * G[j][0] + C1 * G[j][1] + C2 * G[j][2]);
-}
-
 // Link generators 3..5 are reduce_link_PZ's radii: r_e on axis e with exact zeros elsewhere
 // (lane_engine.h emit_link). A product with one of those zeros is ±0 and adding ±0 leaves a sum
 // unchanged, so the terms below drop them: equal to the general arithmetic up to the sign of a
@@ -115,9 +98,11 @@ __device__ inline __attribute__((always_inline)) double dot_z(const double* C, c
     else return C[0] * g[0] + C[1] * g[1] + C[2] * g[2];
 }
 
-// mixed plane of obstacle generator ga and link generator gb = G[BUF_GEN - 6 + j] (the arithmetic
-// of plane_of): E < 0 for a box generator, E = j - 3 for radius E. del sums |A . g_k| over the 9
-// buffered generators in order; the radius terms are A_f r_f (none for f = E, where A_E = 0)
+// plane of obstacle generator ga and link generator gb (CollisionChecking.cu:136-228): the
+// normalised cross product (zero for a parallel pair), d = A . c_obs and delta = sum_k |A . g_k| over
+// the 9 buffered generators in order (the obstacle's 3, the link's 3 box generators and 3 radii).
+// E < 0 for a box generator gb, E = e for radius e; the radius terms are A_f r_f (none for f = E,
+// where A_E = 0)
 template <int E>
 __device__ inline __attribute__((always_inline)) void mixed_plane(const double* ga, const double* gb, const double (*G)[3],
                                                                   const double* oc, double* C, double& dd, double& del) {
@@ -168,48 +153,6 @@ __device__ inline __attribute__((always_inline)) double slice_term(double co, in
 }
 
 // ------------------------------------------------------------------------------------------
-// hyperplane p of the buffered obstacle (CollisionChecking.cu:136-228): the 9 generators are the
-// obstacle's 3 and the link's 6 (3 box generators + 3 diagonal radii, reduce_link_PZ); plane p is
-// the normalised cross product of the pair (a, b) of the lexicographic pair table (:26-39),
-// d = A . c_obs, delta = sum_k |A . g_k|. Evaluated where it is used (eval_kernel): recomputing
-// costs ~70 flops per plane, streaming a stored plane 40 B.
-__device__ inline void buffered_plane(const double* ob, const double* lg, int p, double& C0, double& C1, double& C2,
-                                      double& dd, double& del) {
-    int a = 0, rem = p;
-    while (rem >= BUF_GEN - 1 - a) { rem -= BUF_GEN - 1 - a; a++; }
-    const int b = a + 1 + rem;
-    double G[BUF_GEN][3];
-#pragma unroll
-    for (int i = 0; i < OBS_GEN; i++)
-#pragma unroll
-        for (int r = 0; r < 3; r++) G[i][r] = ob[(i + 1) * 3 + r];
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-#pragma unroll
-        for (int r = 0; r < 3; r++) G[OBS_GEN + i][r] = lg[r + 3 * i];
-    double ga[3], gb[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-        ga[r] = G[0][r]; gb[r] = G[1][r];
-    }
-#pragma unroll
-    for (int i = 0; i < BUF_GEN; i++)
-        if (i == a) { ga[0] = G[i][0]; ga[1] = G[i][1]; ga[2] = G[i][2]; }
-#pragma unroll
-    for (int i = 0; i < BUF_GEN; i++)
-        if (i == b) { gb[0] = G[i][0]; gb[1] = G[i][1]; gb[2] = G[i][2]; }
-    const double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
-    const double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
-    const double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
-    const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
-    C0 = 0; C1 = 0; C2 = 0;
-    if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
-    dd = C0 * ob[0] + C1 * ob[1] + C2 * ob[2];
-    del = 0.0;
-#pragma unroll
-    for (int j = 0; j < BUF_GEN; j++) del += fabs(C0 * G[j][0] + C1 * G[j][1] + C2 * G[j][2]);
-}
-
 // constraint bounds (NLPclass.cu:87-165); rows m..m+NF-1 are the box bounds on x
 __global__ void bounds_kernel(NlpDev d) {
     const RobotParams& rp = *d.rp;
@@ -360,7 +303,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     __syncthreads();
     // slices (PZsparse.cu:404-435 value, :477-516 gradient): one thread per output — k = 0 the
     // value, k = 1..7 the derivative in x_{k-1} — summing its terms in monomial order. Powers come
-    // from a per-variable table (ptab, filled with the staging), the very products ipow forms.
+    // from a per-variable table (ptab, filled with the staging), x_j^g as the reference forms it.
     // The NF * 8 torque outputs (the longest sums) fill wave 0 alone, the link outputs start at
     // thread 64: no wave runs both loops.
     const int nlk = NJ * 3 * 8;
