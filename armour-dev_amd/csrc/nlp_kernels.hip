@@ -76,12 +76,13 @@ __device__ inline double row_va(const NlpDev& d, int slot, int w, int r, const d
 }
 
 // normalised cross product of a generator pair, zero for a parallel pair (CollisionChecking.cu:136-228)
-__device__ inline __attribute__((always_inline)) void plane_normal(const double* ga, const double* gb, double& C0,
-                                                                   double& C1, double& C2) {
-    const double gc0 = ga[1] * gb[2] - ga[2] * gb[1];
-    const double gc1 = ga[2] * gb[0] - ga[0] * gb[2];
-    const double gc2 = ga[0] * gb[1] - ga[1] * gb[0];
-    const double nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
+template <typename R>
+__device__ inline __attribute__((always_inline)) void plane_normal(const R* ga, const R* gb, R& C0,
+                                                                   R& C1, R& C2) {
+    const R gc0 = ga[1] * gb[2] - ga[2] * gb[1];
+    const R gc1 = ga[2] * gb[0] - ga[0] * gb[2];
+    const R gc2 = ga[0] * gb[1] - ga[1] * gb[0];
+    const R nrm = sqrt(gc0 * gc0 + gc1 * gc1 + gc2 * gc2);
     C0 = 0; C1 = 0; C2 = 0;
     if (nrm > 0) { C0 = gc0 / nrm; C1 = gc1 / nrm; C2 = gc2 / nrm; }
 }
@@ -90,8 +91,8 @@ __device__ inline __attribute__((always_inline)) void plane_normal(const double*
 // (lane_engine.h emit_link). A product with one of those zeros is ±0 and adding ±0 leaves a sum
 // unchanged, so the terms below drop them: equal to the general arithmetic up to the sign of a
 // zero. E >= 0 marks a normal whose component E is zero (a plane spanned with radius E).
-template <int E>
-__device__ inline __attribute__((always_inline)) double dot_z(const double* C, const double* g) {
+template <int E, typename R>
+__device__ inline __attribute__((always_inline)) R dot_z(const R* C, const R* g) {
     if constexpr (E == 0) return C[1] * g[1] + C[2] * g[2];
     else if constexpr (E == 1) return C[0] * g[0] + C[2] * g[2];
     else if constexpr (E == 2) return C[0] * g[0] + C[1] * g[1];
@@ -103,18 +104,18 @@ __device__ inline __attribute__((always_inline)) double dot_z(const double* C, c
 // the 9 buffered generators in order (the obstacle's 3, the link's 3 box generators and 3 radii).
 // E < 0 for a box generator gb, E = e for radius e; the radius terms are A_f r_f (none for f = E,
 // where A_E = 0)
-template <int E>
-__device__ inline __attribute__((always_inline)) void mixed_plane(const double* ga, const double* gb, const double (*G)[3],
-                                                                  const double* oc, double* C, double& dd, double& del) {
-    double gc[3];
-    double nrm;
+template <int E, typename R>
+__device__ inline __attribute__((always_inline)) void mixed_plane(const R* ga, const R* gb, const R (*G)[3],
+                                                                  const R* oc, R* C, R& dd, R& del) {
+    R gc[3];
+    R nrm;
     if constexpr (E < 0) {
         gc[0] = ga[1] * gb[2] - ga[2] * gb[1];
         gc[1] = ga[2] * gb[0] - ga[0] * gb[2];
         gc[2] = ga[0] * gb[1] - ga[1] * gb[0];
         nrm = sqrt(gc[0] * gc[0] + gc[1] * gc[1] + gc[2] * gc[2]);
     } else {
-        const double r = gb[E];
+        const R r = gb[E];
         if constexpr (E == 0) { gc[0] = 0.0; gc[1] = ga[2] * r; gc[2] = -(ga[1] * r); }
         else if constexpr (E == 1) { gc[0] = -(ga[2] * r); gc[1] = 0.0; gc[2] = ga[0] * r; }
         else { gc[0] = ga[1] * r; gc[1] = -(ga[0] * r); gc[2] = 0.0; }
@@ -142,8 +143,9 @@ __device__ inline __attribute__((always_inline)) void mixed_plane(const double* 
 // LDS read per factor instead of a select chain (eval_kernel is VALU-issue bound). The reference
 // skips a term whose derivative variable has degree 0; here its factor ptab[k-1][4] = 0 makes the
 // term ±0 (coefficients and x are finite), and adding ±0 is the skip up to the sign of a zero.
-__device__ inline __attribute__((always_inline)) double slice_term(double co, int h, int k, const double (*ptab)[8]) {
-    double v = co;
+template <typename R>
+__device__ inline __attribute__((always_inline)) R slice_term(R co, int h, int k, const R (*ptab)[8]) {
+    R v = co;
 #pragma unroll
     for (int j = 0; j < NF; j++) {
         const int g = (h >> (2 * j)) & 3;
@@ -224,7 +226,8 @@ __device__ double wrap_to_pi(double a) {
 // armour_eval_constraints); mode 1: the line-search trial ws.xt into the non-current slot (worlds
 // still searching only). The sliced link centres go to the slot's own region (feasible_kernel
 // copies the current slot's, the final iterate's, out).
-__global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) {
+template <typename R>
+__global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
     const int t = blockIdx.x, w = blockIdx.y;
     WorldState& S = d.ws[w];
     if (mode == 1 && !(S.status == 0 && S.searching)) return;
@@ -234,32 +237,33 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     const long jt = (long)w * d.T + t;
     const int NJ = d.NJ, O = d.O;
     // everything this (world, t) reads is staged into LDS with coalesced loads first
-    __shared__ double x[NF];
-    __shared__ double lc[MAX_J][3];
-    __shared__ double dlc[MAX_J][NF][3];
-    __shared__ double lgen[MAX_J][18];
-    __shared__ double obs[MAX_OBS][12];
+    __shared__ double x[NF];   // the point itself stays fp64 (cost and extremum rows)
+    __shared__ R lc[MAX_J][3];
+    __shared__ R dlc[MAX_J][NF][3];
+    __shared__ R lgen[MAX_J][18];
+    __shared__ R obs[MAX_OBS][12];
     __shared__ uint16_t lh[MAX_J][CAP_LM];
     __shared__ uint16_t th[NF][CAP_UM];
     // monomial coefficients while slicing; afterwards the same LDS holds the obstacle-independent
     // link-link planes and the link-independent obstacle-obstacle planes
     __shared__ double ubuf[MAX_J * CAP_LM * 3 + NF * CAP_UM];
-    auto lco = reinterpret_cast<double (*)[CAP_LM][3]>(ubuf);
-    auto tco = reinterpret_cast<double (*)[CAP_UM]>(ubuf + MAX_J * CAP_LM * 3);
+    auto lco = reinterpret_cast<R (*)[CAP_LM][3]>(ubuf);
+    auto tco = reinterpret_cast<R (*)[CAP_UM]>(ubuf + MAX_J * CAP_LM * 3);
     constexpr int NMIX = MAX_J * MAX_OBS * OBS_GEN;
     static_assert(MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5 + NMIX + (NMIX + 7) / 8 <= MAX_J * CAP_LM * 3 + NF * CAP_UM,
                   "plane tables");
-    auto llp = reinterpret_cast<double (*)[LL_PLANES][10]>(ubuf);
-    auto oop = reinterpret_cast<double (*)[OO_PLANES][5]>(ubuf + MAX_J * LL_PLANES * 10);
-    double* mixv = ubuf + MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5;   // per (link, obstacle, i)
+    auto llp = reinterpret_cast<R (*)[LL_PLANES][10]>(ubuf);
+    auto oop = reinterpret_cast<R (*)[OO_PLANES][5]>(ubuf + MAX_J * LL_PLANES * 10);
+    R* mixv = reinterpret_cast<R*>(ubuf + MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5);   // per (link, obstacle, i)
     int8_t* mixc = reinterpret_cast<int8_t*>(mixv + NMIX);
     __shared__ int lcnt[MAX_J], tcnt[NF];
-    __shared__ double ptab[NF][8];
+    __shared__ R ptab[NF][8];
     if (tid < NF) {
-        const double xj = mode == 1 ? S.xt[tid] : S.x[tid];
-        x[tid] = xj;
-        ptab[tid][0] = 1.0; ptab[tid][1] = xj; ptab[tid][2] = xj * xj; ptab[tid][3] = xj * xj * xj;
-        ptab[tid][4] = 0.0; ptab[tid][5] = 1.0 * 1.0; ptab[tid][6] = 2.0 * xj; ptab[tid][7] = 3.0 * (xj * xj);
+        const double xd = mode == 1 ? S.xt[tid] : S.x[tid];
+        x[tid] = xd;
+        const R xj = (R)xd;
+        ptab[tid][0] = (R)1.0; ptab[tid][1] = xj; ptab[tid][2] = xj * xj; ptab[tid][3] = xj * xj * xj;
+        ptab[tid][4] = (R)0.0; ptab[tid][5] = (R)1.0 * (R)1.0; ptab[tid][6] = (R)2.0 * xj; ptab[tid][7] = (R)3.0 * (xj * xj);
     }
     if (tid < NJ) lcnt[tid] = d.ro.link_cnt[jt * NJ + tid];
     if (tid >= 32 && tid < 32 + NF) tcnt[tid - 32] = d.ro.tq_cnt[jt * NF + tid - 32];
@@ -312,15 +316,15 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         const int ul = u - 64;
         const int l = ul / 24, e = (ul / 8) % 3, k = ul % 8;
         const long base = jt * NJ + l;
-        double c = k == 0 ? d.ro.link_center[base * 3 + e] : 0.0;
+        R c = k == 0 ? d.ro.link_center[base * 3 + e] : 0.0;
         const int cnt = lcnt[l];
         for (int q = 0; q < cnt; q++) {
             const int h = lh[l][q];
             c = c + slice_term(lco[l][q][e], h, k, ptab);
         }
         if (k == 0) {
-            const double r = d.ro.link_rad[base * 3 + e];
-            const double cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
+            const R r = d.ro.link_rad[base * 3 + e];
+            const R cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
             lc[l][e] = cc;
             d.link_c[slot * d.lcs + base * 3 + e] = cc;
         } else {
@@ -331,12 +335,12 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         if (u >= NF * 8) continue;
         const int j = u / 8, k = u % 8;
         const long base = jt * NF + j;
-        double c = k == 0 ? d.ro.tq_center[base] : 0.0;
+        R c = k == 0 ? d.ro.tq_center[base] : 0.0;
         const int cnt = tcnt[j];
         for (int q = 0; q < cnt; q++) c = c + slice_term(tco[j][q], th[j][q], k, ptab);
         const long gi = gidx(d, slot, w, (long)t * NF + j);
         if (k == 0) {
-            const double r = d.ro.tq_rad[base];
+            const R r = d.ro.tq_rad[base];
             d.g[gi] = ((c - r) + (c + r)) * 0.5;
         } else {
             d.J[gi * NF + k - 1] = c;
@@ -406,11 +410,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
             int i = 0, rem = p;
             while (rem >= 5 - i) { rem -= 5 - i; i++; }
             const int j = i + 1 + rem;
-            const double* ga = &lgen[l][3 * i];
-            const double* gb = &lgen[l][3 * j];
-            double A0, A1, A2;
+            const R* ga = &lgen[l][3 * i];
+            const R* gb = &lgen[l][3 * j];
+            R A0, A1, A2;
             plane_normal(ga, gb, A0, A1, A2);
-            double* P = llp[l][p];
+            R* P = llp[l][p];
             P[0] = A0; P[1] = A1; P[2] = A2;
             P[3] = A0 * lc[l][0] + A1 * lc[l][1] + A2 * lc[l][2];
 #pragma unroll
@@ -418,12 +422,12 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         } else {
             const int v = u - NJ * LL_PLANES, o = v / OO_PLANES, p = v % OO_PLANES;
             const int i = p == 2 ? 1 : 0, j = p == 0 ? 1 : 2;
-            double A0, A1, A2;
+            R A0, A1, A2;
             plane_normal(&obs[o][3 * (i + 1)], &obs[o][3 * (j + 1)], A0, A1, A2);
-            double* P = oop[o][p];
+            R* P = oop[o][p];
             P[0] = A0; P[1] = A1; P[2] = A2;
             P[3] = A0 * obs[o][0] + A1 * obs[o][1] + A2 * obs[o][2];
-            double del = 0.0;
+            R del = 0.0;
 #pragma unroll
             for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * obs[o][3 * (k + 1)] + A1 * obs[o][3 * (k + 1) + 1] + A2 * obs[o][3 * (k + 1) + 2]);
             P[4] = del;
@@ -436,8 +440,8 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     const int nmix = coll ? NJ * O * OBS_GEN : 0;
     for (int u = tid; u < nmix; u += blockDim.x) {
         const int l = u / (O * OBS_GEN), o = (u / OBS_GEN) % O, i = u % OBS_GEN;
-        const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
-        double G[BUF_GEN][3], oc[3];
+        const R c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
+        R G[BUF_GEN][3], oc[3];
 #pragma unroll
         for (int r = 0; r < 3; r++) oc[r] = obs[o][r];
 #pragma unroll
@@ -448,20 +452,20 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         for (int q = 0; q < 6; q++)
 #pragma unroll
             for (int r = 0; r < 3; r++) G[OBS_GEN + q][r] = lgen[l][r + 3 * q];
-        double ga[3];
+        R ga[3];
 #pragma unroll
         for (int r = 0; r < 3; r++) ga[r] = obs[o][(i + 1) * 3 + r];
-        const double cc[3] = {c0, c1, c2};
-        double best = -100000000.0;
+        const R cc[3] = {c0, c1, c2};
+        R best = -100000000.0;
         int code = -1;
         auto scan = [&](auto e_tag, int j) {
             constexpr int E = decltype(e_tag)::value;
-            double A[3], dd, del;
+            R A[3], dd, del;
             mixed_plane<E>(ga, G[OBS_GEN + j], G, oc, A, dd, del);
-            const double Ac = dot_z<E>(A, cc);
+            const R Ac = dot_z<E>(A, cc);
             if (A[0] != 0 || A[1] != 0 || A[2] != 0) {
-                const double pos = Ac - (dd + del);
-                const double neg = -Ac - (-dd + del);
+                const R pos = Ac - (dd + del);
+                const R neg = -Ac - (-dd + del);
                 if (pos > best) { best = pos; code = 2 * j; }
                 if (neg > best) { best = neg; code = 2 * j + 1; }
             }
@@ -483,13 +487,13 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
     // item's first maximum, and a winning mixed plane's normal is formed again at the end
     for (int pr = tid; pr < (coll ? NJ * O : 0); pr += blockDim.x) {
         const int l = pr / O, o = pr % O;
-        double best = -100000000.0;
-        double B0 = 0, B1 = 0, B2 = 0;
+        R best = -100000000.0;
+        R B0 = 0, B1 = 0, B2 = 0;
         bool isneg = false;
         int mwin = -1;  // winning mixed plane: i * 6 + j
-        const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
+        const R c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
         // the 9 buffered generators in registers: obstacle's 3, then the link's 6
-        double G[BUF_GEN][3], oc[3];
+        R G[BUF_GEN][3], oc[3];
 #pragma unroll
         for (int r = 0; r < 3; r++) oc[r] = obs[o][r];
 #pragma unroll
@@ -507,15 +511,15 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
                 if (a < OBS_GEN && b >= OBS_GEN) {
                     if (b == OBS_GEN) {
                         const int u = pr * OBS_GEN + a;
-                        const double v = mixv[u];
+                        const R v = mixv[u];
                         const int cd = mixc[u];
                         if (v > best) { best = v; mwin = a * 6 + (cd >> 1); isneg = cd & 1; }
                     }
                     continue;
                 }
-                double A0, A1, A2, dd, del, Ac;
+                R A0, A1, A2, dd, del, Ac;
                 if (b < OBS_GEN) {
-                    const double* P = oop[o][a + b - 1];
+                    const R* P = oop[o][a + b - 1];
                     A0 = P[0]; A1 = P[1]; A2 = P[2]; dd = P[3]; del = P[4];
 #pragma unroll
                     for (int k = OBS_GEN; k < BUF_GEN - 3; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
@@ -525,7 +529,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
                     Ac = A0 * c0 + A1 * c1 + A2 * c2;
                 } else {
                     const int i = a - OBS_GEN, j = b - OBS_GEN;
-                    const double* P = llp[l][i * (11 - i) / 2 + j - i - 1];
+                    const R* P = llp[l][i * (11 - i) / 2 + j - i - 1];
                     A0 = P[0]; A1 = P[1]; A2 = P[2]; Ac = P[3];
                     dd = A0 * oc[0] + A1 * oc[1] + A2 * oc[2];
                     del = 0.0;
@@ -537,8 +541,8 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
                 // the reference skips a zero normal (norm > 0); for a normalised or zeroed A
                 // that is exactly "some component non-zero"
                 if (A0 != 0 || A1 != 0 || A2 != 0) {
-                    const double pos = Ac - (dd + del);
-                    const double neg = -Ac - (-dd + del);
+                    const R pos = Ac - (dd + del);
+                    const R neg = -Ac - (-dd + del);
                     if (pos > best) { best = pos; B0 = A0; B1 = A1; B2 = A2; isneg = false; mwin = -1; }
                     if (neg > best) { best = neg; B0 = A0; B1 = A1; B2 = A2; isneg = true; mwin = -1; }
                 }
@@ -549,11 +553,17 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel(NlpDev d, int mode) 
         d.g[gi] = -best;
 #pragma unroll
         for (int k = 0; k < NF; k++) {
-            const double dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
+            const R dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
             d.J[gi * NF + k] = isneg ? dot : -dot;
         }
     }
 }
+
+// the product evaluation is fp64; eval_kernel_t<float> serves only the fp32 tolerance study
+// (ARMOUR_EVAL_F32, tools/fp32_study.py): reach sets stay fp64, the slicing and collision
+// arithmetic runs in float
+template __global__ void eval_kernel_t<double>(NlpDev, int);
+template __global__ void eval_kernel_t<float>(NlpDev, int);
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM

@@ -4,7 +4,7 @@
 // T time steps and max_obstacles obstacles, allocated once (the reference allocates per process,
 // KPR/CollisionChecking.cu:17-53). A batch runs entirely on the device:
 //   reach_kernel (JRS + PZ FK/RNEA + torque radius) -> bounds_kernel ->
-//   armour-IPM passes (eval_kernel + ipm_rows_* / ipm_world_*) -> feasible_kernel;
+//   armour-IPM passes (eval_kernel_t + ipm_rows_* / ipm_world_*) -> feasible_kernel;
 // the host only sequences launches and reads one flag word per line-search round.
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -66,6 +66,7 @@ struct armour_planner {
     ReachArgs ra;
     // bundle engine (lane_kernel.hip): default; ARMOUR_ENGINE=job selects the per-job reach_kernel
     bool lane_engine = true;
+    bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
     int lane_grid = 0;
     lane::LaneArgs la;
     // nlp
@@ -201,6 +202,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     {
         const char* eng = std::getenv("ARMOUR_ENGINE");
         p->lane_engine = !(eng && std::strcmp(eng, "job") == 0);
+        const char* f32 = std::getenv("ARMOUR_EVAL_F32");
+        p->eval_f32 = f32 && std::atoi(f32) != 0;
     }
     if (!p->lane_engine) {
         ra.arena_cap = 1 << 17;
@@ -385,13 +388,19 @@ static int nside_count(const armour_planner* p) {
     return 2 * NF * p->T + p->T * p->NJ * p->O + 2 * 4 * NF + 2 * NF;
 }
 
+// g and J of every world of the batch (eval_kernel_t): fp64, or float for the tolerance study
+static void launch_eval(armour_planner* p, dim3 grid, int mode) {
+    if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, grid, dim3(EVAL_THREADS), 0, p->stream, p->d, mode);
+    else hipLaunchKernelGGL(eval_kernel_t<double>, grid, dim3(EVAL_THREADS), 0, p->stream, p->d, mode);
+}
+
 static int run_solver(armour_planner* p) {
     NlpDev& d = p->d;
     const int W = p->W;
     const dim3 rows(d.nblk, W), evg(p->T, W);
     const int wb = (W + 63) / 64;
     hipLaunchKernelGGL(ipm_world_init, dim3(wb), dim3(64), 0, p->stream, d);
-    hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 0);
+    launch_eval(p, evg, 0);
     hipLaunchKernelGGL(ipm_rows_init, rows, dim3(ROW_THREADS), 0, p->stream, d);
     HIPCK(hipGetLastError());
     const int ns = nside_count(p);
@@ -406,7 +415,7 @@ static int run_solver(armour_planner* p) {
         hipLaunchKernelGGL(ipm_world_B, dim3(W), dim3(64), 0, p->stream, d);
         for (int ls = 0; ls < d.opt.max_ls; ls++) {
             p->h_flags[0] = 0;  // no kernel in flight writes it (world_C's last round was synchronised)
-            hipLaunchKernelGGL(eval_kernel, evg, dim3(EVAL_THREADS), 0, p->stream, d, 1);
+            launch_eval(p, evg, 1);
             hipLaunchKernelGGL(ipm_rows_C, rows, dim3(ROW_THREADS), 0, p->stream, d);
             hipLaunchKernelGGL(ipm_world_C, dim3(W), dim3(64), 0, p->stream, d);
             HIPCK(hipStreamSynchronize(p->stream));
@@ -569,7 +578,7 @@ int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g
         ws[i].cur = 0;
     }
     HIPCK(hipMemcpy(d.ws, ws.data(), sizeof(WorldState) * p->W, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(eval_kernel, dim3(p->T, p->W), dim3(EVAL_THREADS), 0, p->stream, d, 0);
+    launch_eval(p, dim3(p->T, p->W), 0);
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(g, d.g + gidx(d, 0, w, 0), sizeof(double) * d.m, hipMemcpyDeviceToHost, p->stream));
     if (jac) HIPCK(hipMemcpyAsync(jac, d.J + gidx(d, 0, w, 0) * NF, sizeof(double) * d.m * NF, hipMemcpyDeviceToHost, p->stream));
