@@ -190,7 +190,7 @@ def main():
     if tr is not None:
         line["roofline"]["traffic"] = tr[1]["traffic_bytes_per_launch"]
         line["roofline"]["traffic_source"] = os.path.relpath(tr[0], ROOT)
-    if a.cpu_seconds > 0:
+    if a.cpu_seconds > 0 and world_size == 1:   # the CPU baseline is an N = 1 figure (rank 0 only)
         rs = None
         if robot is not None:
             from armour_amd import robot_tables as RT
