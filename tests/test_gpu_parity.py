@@ -86,6 +86,13 @@ def test_config2_batch():
     _compare_batch(100, 20, [11, 12, 13, 14], [np.zeros(7), np.array([0.5, 0.6, 0.7, 0.0, -0.5, -0.6, -0.7])])
 
 
+def test_config2_bench_batch_sweep():
+    """BASELINE configs[1] at batch scale: 64 worlds (100 bundles of the reach engine, so bundle
+    boundaries fall inside worlds), every plan against the oracle"""
+    rng = np.random.default_rng(5)
+    _compare_batch(100, 20, list(range(500, 564)), [rng.uniform(-1, 1, 7)])
+
+
 def test_config5_fetch_batch():
     """BASELINE configs[4]: the Fetch arm from its URDF (tests/golden/robot_fetch.json: 7 actuated
     joints + the fixed gripper), here at fp64 and reduced sizes (T=40, O=8); the full-size run is
