@@ -101,6 +101,12 @@ def test_config5_fetch_batch():
     _compare_batch(40, 8, [31, 32, 33], [np.zeros(7), np.linspace(-0.6, 0.6, 7)], robot=fetch)
 
 
+def test_config5_fetch_full_size():
+    """BASELINE configs[4] at its full size (T=100, O=20), fp64"""
+    fetch = RT.load_json(os.path.join(GOLD, "robot_fetch.json"))
+    _compare_batch(100, 20, list(range(600, 616)), [np.full(7, 0.3)], robot=fetch)
+
+
 def test_config3_batch():
     """BASELINE configs[2]: T=200, O=40 (MAX_OBSTACLE_NUM)"""
     _compare_batch(200, 40, [21, 22], [np.full(7, -0.4)])
