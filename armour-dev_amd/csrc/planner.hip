@@ -438,6 +438,21 @@ static int run_solver(armour_planner* p) {
     return 0;
 }
 
+// Every entry point runs on its planner's device, whatever the calling thread's current device is
+// (handles may be driven from other host threads); the caller's device is restored.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(const armour_planner* p) {
+        int cur = -1;
+        if (p && p->cfg.device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != p->cfg.device &&
+            hipSetDevice(p->cfg.device) == hipSuccess)
+            prev = cur;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 extern "C" {
 
 const char* armour_last_error(void) { return g_err.c_str(); }
@@ -472,6 +487,7 @@ armour_planner* armour_create_robot(const armour_config* cfg, const armour_robot
 }
 
 void armour_destroy(armour_planner* p) {
+    DeviceScope device_scope(p);
     if (!p) return;
     if (p->stream) (void)hipStreamSynchronize(p->stream);
     for (void* a : p->allocs) (void)hipFree(a);
@@ -490,6 +506,7 @@ int armour_num_constraints(const armour_planner* p, int O) { return p ? NF * p->
 int armour_num_joints(const armour_planner* p) { return p ? p->NJ : ARMOUR_E_ARG; }
 
 int armour_get_joint_bounds(const armour_planner* p, double* b) {
+    DeviceScope device_scope(p);
     if (!p || !b) return fail(ARMOUR_E_ARG, "null argument");
     const RobotParams& rp = p->rp;
     for (int i = 0; i < NF; i++) {
@@ -502,6 +519,7 @@ int armour_get_joint_bounds(const armour_planner* p, double* b) {
 }
 
 int armour_reach_batch(armour_planner* p, int W, const armour_world* worlds, armour_timing* timing) {
+    DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     p->reached = p->planned = false;
     auto t0 = std::chrono::steady_clock::now();
@@ -524,6 +542,7 @@ int armour_reach_batch(armour_planner* p, int W, const armour_world* worlds, arm
 }
 
 int armour_plan_batch(armour_planner* p, int W, const armour_world* worlds, armour_result* results, armour_timing* timing) {
+    DeviceScope device_scope(p);
     if (!p || !results) return fail(ARMOUR_E_ARG, "null planner / results");
     p->reached = p->planned = false;
     auto t0 = std::chrono::steady_clock::now();
@@ -564,6 +583,7 @@ int armour_plan_batch(armour_planner* p, int W, const armour_world* worlds, armo
 }
 
 int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g, double* jac) {
+    DeviceScope device_scope(p);
     if (!p || !x || !g) return fail(ARMOUR_E_ARG, "null argument");
     if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set: call armour_reach_batch or armour_plan_batch first");
     if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
@@ -588,6 +608,7 @@ int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g
 }
 
 int armour_get_constraints(armour_planner* p, int w, double* g) {
+    DeviceScope device_scope(p);
     if (!p || !g) return fail(ARMOUR_E_ARG, "null argument");
     if (!p->planned) return fail(ARMOUR_E_STATE, "no plan");
     if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
@@ -597,6 +618,7 @@ int armour_get_constraints(armour_planner* p, int w, double* g) {
 }
 
 int armour_get_link_centers(armour_planner* p, int w, double* c) {
+    DeviceScope device_scope(p);
     if (!p || !c) return fail(ARMOUR_E_ARG, "null argument");
     if (!p->planned) return fail(ARMOUR_E_STATE, "no plan");
     if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
@@ -605,6 +627,7 @@ int armour_get_link_centers(armour_planner* p, int w, double* c) {
 }
 
 int armour_get_link_generators(armour_planner* p, int w, double* gens) {
+    DeviceScope device_scope(p);
     if (!p || !gens) return fail(ARMOUR_E_ARG, "null argument");
     if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
     if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
@@ -618,6 +641,7 @@ int armour_get_link_generators(armour_planner* p, int w, double* gens) {
 }
 
 int armour_get_torque_radius(armour_planner* p, int w, double* radius) {
+    DeviceScope device_scope(p);
     if (!p || !radius) return fail(ARMOUR_E_ARG, "null argument");
     if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
     if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
@@ -626,6 +650,7 @@ int armour_get_torque_radius(armour_planner* p, int w, double* radius) {
 }
 
 int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms, int capacity) {
+    DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (!p->d_prof) return fail(ARMOUR_E_STATE, "op profiling is off (set ARMOUR_PROFILE_OPS before armour_create)");
     // capacity in pairs: nops + 8 -> per-op [cycles, terms] + 16 phase totals; nops + 8 + 4 * OP_NCODES
@@ -638,6 +663,7 @@ int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms
 }
 
 int armour_get_reach_dump(armour_planner* p, double* dump, int capacity) {
+    DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (!p->d_dump) return fail(ARMOUR_E_STATE, "op dump is off (set ARMOUR_DUMP_OPS before armour_create)");
     if (dump && capacity >= p->nops) {

@@ -18,6 +18,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -36,6 +37,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=0,
                     help="worlds per GPU per step (0: two whole bundle waves of the device, floor(2 * CUs * 64 / T): "
                          "327 on MI355X at T=100)")
+    ap.add_argument("--planners", type=int, default=2,
+                    help="planners per GPU planning their own --batch concurrently (one HIP stream each, "
+                         "one host thread each); 2 overlaps one planner's solver with the other's reach")
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--O", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
@@ -119,8 +123,36 @@ def main():
         robot = RT.load_json(os.path.join(ROOT, "tests", "golden", "robot_fetch.json"))
         geo = RT.geometry(robot)
         robot_name = "Fetch arm (URDF, 7 actuated + fixed gripper)"
-    worlds = [A.make_world(i, a.O, robot=geo) for i in D.shard(a.batch * world_size, rank, world_size)]
-    planner = A.Planner(T=a.T, max_obstacles=a.O, max_worlds=a.batch, device=local_rank, robot=robot)
+    # a.planners planners per GPU (one HIP stream each) plan their own batch concurrently from host
+    # threads (ctypes releases the GIL in armour_plan_batch); the GPU overlaps one planner's solver
+    # iterations with another's reach. The rank's worlds are split between them.
+    P = a.planners
+    worlds_all = [A.make_world(i, a.O, robot=geo) for i in D.shard(a.batch * P * world_size, rank, world_size)]
+    subs = [worlds_all[p * a.batch:(p + 1) * a.batch] for p in range(P)]
+    worlds = subs[0]
+    planners = [A.Planner(T=a.T, max_obstacles=a.O, max_worlds=a.batch, device=local_rank, robot=robot)
+                for _ in range(P)]
+    planner = planners[0]
+
+    def plan_all():
+        # one step: every planner plans its batch; the collective below stays on this thread, so
+        # every rank issues it in the same order
+        if P == 1:
+            res, tm = planner.plan(worlds)
+            return res, [tm]
+        out = [None] * P
+
+        def work(p):
+            out[p] = planners[p].plan(subs[p])
+
+        ths = [threading.Thread(target=work, args=(p,)) for p in range(P)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        if any(o is None for o in out):
+            raise RuntimeError("a planner thread failed")
+        return [r for o in out for r in o[0]], [o[1] for o in out]
 
     def gather(res):
         return D.gather(D.records(res), dist, device="cuda" if dist is not None else None)
@@ -133,15 +165,15 @@ def main():
             torch.cuda.synchronize()
 
     for _ in range(a.warmup):
-        res, tm = planner.plan(worlds)
+        res, _ = plan_all()
         gather(res)
     barrier()
     t0 = time.perf_counter()
     tms = []
     for _ in range(a.steps):
-        res, tm = planner.plan(worlds)
+        res, tm = plan_all()
         allrec, best = gather(res)
-        tms.append(tm)
+        tms.extend(tm)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -153,7 +185,7 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
-    total_plans = a.steps * a.batch * world_size
+    total_plans = a.steps * a.batch * P * world_size
     # roofline of the dominant kernel (reach_kernel): algorithmic bytes = monomial bytes read and
     # written by the PZ operators, timed with HIP events on the planner stream
     rk_ms = float(np.mean([t["reach_kernel_ms"] for t in tms]))
@@ -173,8 +205,11 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic random-obstacle worlds (armour_amd.worlds, seeds rank*batch+i)",
-        "config": {"workload": f"{robot_name}, T={a.T}, O={a.O} box obstacles, {a.batch} worlds/GPU/step",
-                   "num_time_steps": a.T, "obstacles": a.O, "worlds_per_gpu": a.batch,
+        "config": {"workload": f"{robot_name}, T={a.T}, O={a.O} box obstacles, "
+                               + (f"{a.batch} worlds/GPU/step" if P == 1 else
+                                  f"{P} concurrent planners x {a.batch} worlds/GPU/step"),
+                   "num_time_steps": a.T, "obstacles": a.O, "worlds_per_gpu": a.batch * P,
+                   "planners_per_gpu": P, "worlds_per_planner": a.batch,
                    "parallelism": f"world-sharded x{world_size}, RCCL all_gather of per-world records"},
         "breakdown_ms": {"reach": float(np.mean([t["reach_ms"] for t in tms])),
                          "nlp": float(np.mean([t["nlp_ms"] for t in tms])),

@@ -63,3 +63,28 @@ def test_argument_and_state_errors():
     P.plan(worlds[:2])
     with pytest.raises(A.ArmourError, match="out of range"):
         P.torque_radius(2)
+
+
+def test_concurrent_planners_match_sequential():
+    # bench.py's default: planners driven from their own host threads (one HIP stream each) must
+    # give, world by world, bitwise the results of sequential planning
+    import threading
+    W, T, O = 6, 40, 8
+    batches = [[A.make_world(700 + 10 * b + s, O) for s in range(W)] for b in range(2)]
+    seq = [A.Planner(T=T, max_obstacles=O, max_worlds=W).plan(bw)[0] for bw in batches]
+    planners = [A.Planner(T=T, max_obstacles=O, max_worlds=W) for _ in range(2)]
+    out = [None, None]
+
+    def work(b):
+        out[b] = planners[b].plan(batches[b])[0]
+
+    ths = [threading.Thread(target=work, args=(b,)) for b in range(2)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    for b in range(2):
+        assert out[b] is not None
+        for r0, r1 in zip(seq[b], out[b]):
+            assert np.array_equal(r0["k_opt"], r1["k_opt"]) and r0["iterations"] == r1["iterations"]
+            assert r0["feasible"] == r1["feasible"] and r0["status"] == r1["status"]
