@@ -21,6 +21,9 @@ _LIB = None
 _dp = ctypes.POINTER(ctypes.c_double)
 
 
+ARMOUR_E_ARG, ARMOUR_E_HIP, ARMOUR_E_CAPACITY, ARMOUR_E_STATE = -1, -2, -3, -4  # include/armour_hip.h
+
+
 class ArmourError(RuntimeError):
     pass
 
@@ -45,7 +48,7 @@ _WORLD_DTYPE = np.dtype({"names": ["q0", "qd0", "qdd0", "q_des", "num_obstacles"
 class Result(ctypes.Structure):
     _fields_ = [("k_opt", ctypes.c_double * NF), ("feasible", ctypes.c_int), ("solver_status", ctypes.c_int),
                 ("iterations", ctypes.c_int), ("evaluations", ctypes.c_int), ("cost", ctypes.c_double),
-                ("kkt_error", ctypes.c_double)]
+                ("kkt_error", ctypes.c_double), ("error", ctypes.c_int)]
 
 
 class Timing(ctypes.Structure):
@@ -77,6 +80,8 @@ def lib():
         L.armour_reach_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Timing)]
         L.armour_eval_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
         L.armour_get_reach_program.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.armour_get_reach_occupancy.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
+                                                 ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.armour_get_joint_bounds.argtypes = [ctypes.c_void_p, _dp]
         L.armour_get_reach_dump.argtypes = [ctypes.c_void_p, _dp, ctypes.c_int]
         L.armour_get_reach_profile.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
@@ -92,7 +97,7 @@ ABI_SYMBOLS = ["armour_create", "armour_create_robot", "armour_robot_builtin", "
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
-               "armour_get_reach_dump"]
+               "armour_get_reach_dump", "armour_get_reach_occupancy"]
 
 
 def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
@@ -169,7 +174,8 @@ class Planner:
         out = []
         for r in res:
             out.append(dict(k_opt=np.array(r.k_opt[:]), feasible=bool(r.feasible), status=r.solver_status,
-                            iterations=r.iterations, evaluations=r.evaluations, cost=r.cost, kkt=r.kkt_error))
+                            iterations=r.iterations, evaluations=r.evaluations, cost=r.cost, kkt=r.kkt_error,
+                            error=r.error))
         return out, tm.as_dict()
 
     def reach(self, worlds):
@@ -236,10 +242,22 @@ class Planner:
         a = np.array(buf[:], dtype=np.uint64)
         return a[:2 * n].reshape(n, 2), a[2 * n:]
 
+    OCCUPANCY = ("arena_hashes", "arena_rows", "operator_terms", "link_monomials", "torque_monomials",
+                 "worlds_retried", "worlds_failed")
+
+    def occupancy(self):
+        """{name: (largest use in the last reach, capacity)} (armour_get_reach_occupancy)"""
+        n = len(self.OCCUPANCY)
+        used = (ctypes.c_longlong * n)()
+        caps = (ctypes.c_longlong * n)()
+        rc = lib().armour_get_reach_occupancy(self.h, used, caps, n)
+        _check(min(0, rc))
+        return {k: (int(used[i]), int(caps[i])) for i, k in enumerate(self.OCCUPANCY)}
+
     def torque_radius(self, w):
         r = np.zeros((self.T, NF))
         _check(lib().armour_get_torque_radius(self.h, w, _ptr(r)))
         return r
 
 
-__all__ = ["Planner", "ArmourError", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]
+__all__ = ["Planner", "ArmourError", "ARMOUR_E_CAPACITY", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]

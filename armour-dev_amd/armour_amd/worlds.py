@@ -61,14 +61,25 @@ def link_spheres(robot: Robot, q: np.ndarray):
     return np.array(cs), np.array(rs)
 
 
-def make_world(seed: int, num_obstacles: int, robot: Robot = KINOVA):
+PROFILES = ("default", "survey")
+
+
+def make_world(seed: int, num_obstacles: int, robot: Robot = KINOVA, profile: str = "default"):
+    """profile "default": the generator above (half ranges, 5 cm clearance at the start);
+    "survey": SURVEY §8(d) exactly — qd0 ~ U(-0.5, 0.5) * speed_limit, qdd0 ~ U(-1, 1), obstacles
+    rejected only when they intersect the start configuration (no clearance margin). About a third
+    of the "survey" worlds are over the torque limits at k = 0."""
+    if profile not in PROFILES:
+        raise ValueError(f"unknown world profile {profile!r}")
     rng = np.random.default_rng(seed)
     n = 7
     lb = np.where(robot.state_lb < -100, -np.pi, robot.state_lb + 0.2)
     ub = np.where(robot.state_ub > 100, np.pi, robot.state_ub - 0.2)
     q0 = rng.uniform(lb, ub)
-    qd0 = rng.uniform(-0.25, 0.25, n) * robot.speed_limits
-    qdd0 = rng.uniform(-0.5, 0.5, n)
+    f = 1.0 if profile == "survey" else 0.5
+    margin = 0.0 if profile == "survey" else 0.05
+    qd0 = rng.uniform(-0.5 * f, 0.5 * f, n) * robot.speed_limits
+    qdd0 = rng.uniform(-f, f, n)
     q_des = q0 + rng.uniform(-1.0, 1.0, n) * (np.pi / 48) * 0.8
     centres, radii = link_spheres(robot, q0)
     obs = []
@@ -82,7 +93,7 @@ def make_world(seed: int, num_obstacles: int, robot: Robot = KINOVA):
         c = rng.uniform(lo, hi)
         if tries < 100000:
             r_obs = float(np.linalg.norm(side / 2))
-            if np.any(np.linalg.norm(centres - c, axis=1) < radii + r_obs + 0.05):
+            if np.any(np.linalg.norm(centres - c, axis=1) < radii + r_obs + margin):
                 continue
         g = np.diag(side / 2)
         obs.append(np.concatenate([c, g[:, 0], g[:, 1], g[:, 2]]))

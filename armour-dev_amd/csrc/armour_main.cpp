@@ -101,6 +101,9 @@ int main(int argc, char** argv) {
     }
     std::cout << "        HIP: reachable sets " << tm.reach_ms << " ms, solver " << tm.nlp_ms << " ms, "
               << (r.feasible ? "found a feasible solution" : "no feasible solution") << std::endl;
+    // a reach set over the library's capacity is not planned: reported as no feasible solution
+    // (-1, MATLAB keeps its braking trajectory), with the reason on stderr
+    if (r.error) std::fprintf(stderr, "        armour_main: %s\n", armour_last_error());
 
     const int NJ = armour_num_joints(p);
     const int m = armour_num_constraints(p, O);

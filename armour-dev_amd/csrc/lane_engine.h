@@ -88,6 +88,8 @@ struct LCtx {
     double* scr;           // LDS [2 * NF][LG]: per-job disturbance / reduce radii
     int* iscan;            // LDS [LW]
     int* err;              // LDS
+    int* occ;              // LDS [4]: largest operator term count, link / torque k-only monomials,
+                           // arena coefficient rows in use
     double thr;
     const JrsJoint* jrs;   // this lane's job: jrs[i], i < NF
     unsigned long long* prof;  // optional per-op [cycles, terms] + phase cycles (null: off)
@@ -143,6 +145,7 @@ DI bool arena_alloc(const LCtx& x, LH& h, int K, int stride) {
     const long h0 = (long)atomicAdd((unsigned long long*)&x.A->hused, (unsigned long long)K);
     const long c0 = (long)atomicAdd((unsigned long long*)&x.A->cused, (unsigned long long)K * stride);
     h.stride = stride;
+    atomicMax(&x.occ[3], (int)min(c0 + (long)K * stride, (long)INT_MAX));
     if (h0 + K > x.A->hcap || c0 + (long)K * stride > x.A->ccap) {
         err_or(x, ERR_ARENA);
         h.cnt = 0; h.hoff = 0; h.coff = 0;
@@ -743,6 +746,7 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
     double red[Pol::NR];
 #pragma unroll
     for (int e = 0; e < Pol::NR; e++) red[e] = 0.0;
+    if (x.tid == 0) atomicMax(&x.occ[0], N);
     if (N > x.cap_glb || N >= (1 << 16)) {
         if (x.tid == 0) { err_or(x, ERR_SORTCAP); x.H[o].cnt = 0; }
         combine_red<Pol::NR>(x, red);
@@ -900,6 +904,7 @@ DI void cross_const(LCtx& x, int o, int a, const CrossC& C) {
 #pragma unroll
     for (int e = 0; e < 9; e++) red[e] = 0.0;
     int* kp = N <= x.cap_lds ? x.kp : x.gkp;
+    if (x.tid == 0) atomicMax(&x.occ[0], N);
     if (N > x.cap_glb || N > x.cap_out) {
         if (x.tid == 0) { err_or(x, ERR_SORTCAP); x.H[o].cnt = 0; }
         combine_red<9>(x, red);
@@ -1207,6 +1212,7 @@ DI void emit_link(const LCtx& x, const ReachOut& out, int a, int l) {
     double* gens = out.link_gens + base * 18;
 #pragma unroll
     for (int e = 0; e < 18; e++) gens[e] = gl[e];
+    atomicMax(&x.occ[1], kk);
     out.link_cnt[base] = kk < CAP_LM ? kk : CAP_LM;
 #pragma unroll
     for (int e = 0; e < 3; e++) { out.link_center[base * 3 + e] = cen(x, h, e); out.link_rad[base * 3 + e] = rad[e]; }
@@ -1241,6 +1247,7 @@ DI void emit_torque(const LCtx& x, const ReachOut& out, int a, int i) {
     if (bad && x.valid) err_or(x, bad);
     x.scr[(long)(NF + i) * LG + x.lane] = rad;
     if (!x.valid) return;
+    atomicMax(&x.occ[2], kk);
     out.tq_cnt[base] = kk < CAP_UM ? kk : CAP_UM;
     out.tq_center[base] = cen(x, h, 0);
     out.tq_rad[base] = rad;

@@ -34,6 +34,10 @@ struct LaneArgs {
     unsigned long long* bytes;
     double* dump;          // optional [nops][DUMP_W][LG] of bundle 0 (null: off)
     unsigned long long* prof;  // optional [2 * nops + 16] per-op cycles/terms + phase cycles
+    unsigned long long* occ;   // [8] largest use over the launch: arena hashes, arena rows, operator
+                               // terms, link / torque k-only monomials (capacity headroom)
+    const int* wlist;      // null: every world of the batch; else only these worlds (a retry)
+    int nlist;
 };
 
 #ifndef LANE_CFG_WPE
@@ -53,6 +57,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     __shared__ int iscan[LW];
     __shared__ LArena arena;
     __shared__ int err;
+    __shared__ int occ[4];
 
     const RobotParams& rp = *rpp;
     const long wg = blockIdx.x;
@@ -79,11 +84,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     x.scr = scr;
     x.iscan = iscan;
     x.err = &err;
+    x.occ = occ;
     x.thr = rp.simplify_threshold;
     x.prof = a.prof;
     x.nops = a.nops;
 
-    const long njobs = (long)a.W * a.T;
+    // a retry (wlist) runs the listed worlds' jobs only, as consecutive bundles of their own
+    const long njobs = (long)(a.wlist ? a.nlist : a.W) * a.T;
     const long nb = (njobs + LG - 1) / LG;
     for (long b = blockIdx.x; b < nb; b += gridDim.x) {
         if (x.tid == 0) {
@@ -96,17 +103,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
             arena.cused = 0;
             arena.bytes = 0;
             err = 0;
+            occ[0] = occ[1] = occ[2] = occ[3] = 0;
         }
         for (int k = x.tid; k < a.nslots; k += LT) H[k].off = a.slot_off[k];
-        const long job = b * LG + x.lane;
+        long job = b * LG + x.lane;
         x.valid = job < njobs;
-        x.job = x.valid ? job : njobs - 1;
+        job = x.valid ? job : njobs - 1;
+        x.job = a.wlist ? (long)a.wlist[job / a.T] * a.T + job % a.T : job;
         x.jrs = a.jrs + x.job * NF;
         __syncthreads();
         run_program(x, rp, a.prog, a.nops, out, b == 0 ? a.dump : nullptr);
         __syncthreads();
         if (err && x.wave == 0 && x.valid) atomicOr(&out.err[x.job / a.T], err);
-        if (x.tid == 0) atomicAdd(a.bytes, arena.bytes);
+        if (x.tid == 0) {
+            atomicAdd(a.bytes, arena.bytes);
+            atomicMax(&a.occ[0], (unsigned long long)arena.hused);
+            atomicMax(&a.occ[1], (unsigned long long)max((long)occ[3], arena.cused));
+            for (int k = 0; k < 3; k++) atomicMax(&a.occ[2 + k], (unsigned long long)occ[k]);
+        }
         __syncthreads();
     }
 }

@@ -34,7 +34,7 @@ struct WorldState {
     double filt_theta[MAX_FILTER], filt_phi[MAX_FILTER];
     int nfilt;
     int cur;           // eval slot holding the current point
-    int status;        // 0 running, 1 converged, 2 max_iter, 3 line-search failure
+    int status;        // 0 running, 1 converged, 2 max_iter, 3 line-search failure, 4 reach over capacity
     int searching;     // 1 while the line search of this iteration has not accepted
     int accepted_ok;   // last acceptance passed the filter (0: forced after max_ls trials)
     int ftype;

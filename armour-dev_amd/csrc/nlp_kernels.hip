@@ -584,7 +584,7 @@ __global__ void ipm_world_init(NlpDev d) {
     S.theta_min = -1;
     S.nfilt = 0;
     S.cur = 0;
-    S.status = 0;
+    S.status = d.ro.err[w] ? 4 : 0;  // 4: reach set over capacity (planner.hip run_reach), not planned
     S.searching = 0;
     S.first_update = 1;
     S.nfail = 0;
@@ -1058,7 +1058,7 @@ __global__ void feasible_kernel(NlpDev d, int* feasible) {
     double* dst = d.link_c + 2 * d.lcs + w * n;
     for (long i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
     __syncthreads();
-    if (threadIdx.x == 0) feasible[w] = bad ? 0 : 1;
+    if (threadIdx.x == 0) feasible[w] = (bad || S.status == 4) ? 0 : 1;
 }
 
 }  // namespace armour

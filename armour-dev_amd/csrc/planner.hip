@@ -59,6 +59,10 @@ struct armour_planner {
     unsigned long long* d_prof = nullptr;  // per-op [cycles, terms] when ARMOUR_PROFILE_OPS is set
     double* d_dump = nullptr;              // op-by-op state of job 0 when ARMOUR_DUMP_OPS is set
     double last_kernel_ms = 0, last_bytes = 0;
+    unsigned long long* d_occ = nullptr;   // [8] reach capacity use of the last batch (lane kernel)
+    int* d_wlist = nullptr;                // [max_worlds] worlds of a capacity retry
+    int last_retried = 0, last_failed = 0;
+    std::vector<int> world_err;            // per world of the last batch: 0 or ARMOUR_E_CAPACITY
     // inputs
     double *q0 = nullptr, *qd0 = nullptr, *qdd0 = nullptr, *qdes = nullptr, *obs = nullptr, *xin = nullptr;
     // reach
@@ -100,6 +104,9 @@ static int row_chunk() {
     const int c = e ? std::atoi(e) : 1024;
     return (c >= 256 && c % 256 == 0) ? c : 1024;
 }
+
+// capacity retry: a quarter of the workgroups, each with four workgroups' buffers
+constexpr int RETRY_SCALE = 4;
 
 static int planner_init(armour_planner* p, const armour_config* cfg, const armour_robot* robot) {
     p->cfg = *cfg;
@@ -234,13 +241,18 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             (void)pb.slot_offsets(&pool);
         }
         la.pool_rows = pool + 9;
-        const size_t G = (size_t)p->lane_grid, LGs = lane::LG;
+        // buffers of at least RETRY_SCALE workgroups, so even a one-world batch has a capacity retry
+        const size_t G = (size_t)std::max(p->lane_grid, RETRY_SCALE), LGs = lane::LG;
         if ((rc = p->alloc(&la.pool, G * la.pool_rows * LGs)) || (rc = p->alloc(&la.arena_h, G * la.hcap)) ||
             (rc = p->alloc(&la.arena_m, G * la.hcap)) || (rc = p->alloc(&la.arena_c, G * la.ccap * LGs)) ||
             (rc = p->alloc(&la.gkh, G * la.gcap)) || (rc = p->alloc(&la.gki, G * la.gcap)) ||
             (rc = p->alloc(&la.gkp, G * (la.gcap + 1))) || (rc = p->alloc(&la.ggp, G * (la.gcap + 1))) ||
             (rc = p->alloc(&la.gout, G * la.ocap * 9 * LGs)) || (rc = p->alloc(&la.gm, G * la.ocap)))
             return rc;
+        if ((rc = p->alloc(&p->d_occ, 8)) || (rc = p->alloc(&p->d_wlist, (size_t)Wm))) return rc;
+        la.occ = p->d_occ;
+        la.wlist = nullptr;
+        la.nlist = 0;
         la.prog = p->d_prog;
         la.nops = p->nops;
         la.slot_off = p->d_slot_off;
@@ -339,6 +351,7 @@ static int run_reach(armour_planner* p) {
     ra.qdd0 = p->qdd0;
     HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, p->stream));
     HIPCK(hipMemsetAsync(p->d_bytes, 0, sizeof(unsigned long long), p->stream));
+    if (p->d_occ) HIPCK(hipMemsetAsync(p->d_occ, 0, sizeof(unsigned long long) * 8, p->stream));
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
     const long nj = jobs * NF;
@@ -359,9 +372,6 @@ static int run_reach(armour_planner* p) {
     }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(p->ev[4], p->stream));
-    const long rows = (long)p->W * d.R;
-    hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, p->stream, d);
-    HIPCK(hipGetLastError());
     std::vector<int> err(p->W);
     unsigned long long bytes = 0;
     HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, p->stream));
@@ -373,12 +383,53 @@ static int run_reach(armour_planner* p) {
         p->last_kernel_ms = ms;
         p->last_bytes = (double)bytes;
     }
+    // Capacity isolation. A bundle that overflowed its arena / key buffers flags every world it
+    // holds. Those worlds' jobs run again in a second launch of a quarter of the workgroups, each
+    // with four workgroups' buffers (4x the arena, key and output capacity). A world that still
+    // overflows gets ARMOUR_E_CAPACITY in its result and is not planned; the batch goes on.
+    std::vector<int> retry;
+    for (int w = 0; w < p->W; w++)
+        if (err[w]) retry.push_back(w);
+    p->last_retried = (int)retry.size();
+    if (!retry.empty() && p->lane_engine) {
+        lane::LaneArgs la = p->la;
+        la.W = p->W;
+        la.T = p->T;
+        la.jrs = p->d_jrs;
+        la.hcap *= RETRY_SCALE;
+        la.ccap *= RETRY_SCALE;
+        la.gcap *= RETRY_SCALE;
+        la.ocap *= RETRY_SCALE;
+        la.pool_rows *= RETRY_SCALE;
+        la.wlist = p->d_wlist;
+        la.nlist = (int)retry.size();
+        HIPCK(hipMemcpyAsync(p->d_wlist, retry.data(), sizeof(int) * retry.size(), hipMemcpyHostToDevice, p->stream));
+        HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, p->stream));
+        const long bundles = ((long)retry.size() * p->T + lane::LG - 1) / lane::LG;
+        const long g = std::max(p->lane_grid, RETRY_SCALE) / RETRY_SCALE;
+        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3((int)(bundles < g ? bundles : g)), dim3(lane::LT), 0, p->stream,
+                           p->d_rp, la, p->ro);
+        HIPCK(hipGetLastError());
+        HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, p->stream));
+        HIPCK(hipStreamSynchronize(p->stream));
+    }
+    // constraint bounds from the (final) torque radii
+    const long rows = (long)p->W * d.R;
+    hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, p->stream, d);
+    HIPCK(hipGetLastError());
+    p->world_err.assign(p->W, 0);
+    p->last_failed = 0;
     for (int w = 0; w < p->W; w++)
         if (err[w]) {
-            char buf[160];
-            std::snprintf(buf, sizeof(buf), "reach-set job of world %d exceeded a capacity (error bits 0x%x)", w, err[w]);
-            return fail(ARMOUR_E_CAPACITY, buf);
+            p->world_err[w] = ARMOUR_E_CAPACITY;
+            p->last_failed++;
         }
+    if (p->last_failed) {
+        char buf[200];
+        std::snprintf(buf, sizeof(buf), "%d world(s) exceeded a reach-set capacity (first: world %d); the rest are planned",
+                      p->last_failed, (int)(std::find_if(err.begin(), err.end(), [](int e) { return e != 0; }) - err.begin()));
+        g_err = buf;
+    }
     p->reached = true;
     return 0;
 }
@@ -476,6 +527,12 @@ armour_planner* armour_create(const armour_config* cfg) { return armour_create_r
 
 armour_planner* armour_create_robot(const armour_config* cfg, const armour_robot* robot) {
     if (!cfg) { fail(ARMOUR_E_ARG, "null config"); return nullptr; }
+    // planner_init makes cfg->device current; the caller's current device is restored on return
+    struct Restore {
+        int dev = -1;
+        Restore() { if (hipGetDevice(&dev) != hipSuccess) dev = -1; }
+        ~Restore() { if (dev >= 0) (void)hipSetDevice(dev); }
+    } restore;
     armour_planner* p = new armour_planner();
     if (planner_init(p, cfg, robot) != 0) {
         std::string keep = g_err;
@@ -562,11 +619,16 @@ int armour_plan_batch(armour_planner* p, int W, const armour_world* worlds, armo
         armour_result& r = results[w];
         for (int i = 0; i < NF; i++) r.k_opt[i] = S.x[i];
         r.feasible = p->h_feas[w];
-        r.solver_status = S.status == 1 ? 0 : S.status == 2 ? 1 : 2;
+        r.solver_status = S.status == 1 ? 0 : S.status == 2 ? 1 : S.status == 3 ? 2 : 3;
         r.iterations = S.iter;
         r.evaluations = S.nevals;
         r.cost = p->h_f[S.cur * p->d.W + w] / p->rp.cost_scale;
         r.kkt_error = S.kkt;
+        r.error = p->world_err[w];
+        if (r.error) {
+            r.solver_status = 3;
+            r.feasible = 0;
+        }
     }
     p->planned = true;
     if (timing) {
@@ -590,14 +652,16 @@ int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g
     NlpDev& d = p->d;
     // evaluate every world of the batch at x in slot 0 (ws.x is the solver's start/end point, so
     // a subsequent query of solver outputs must re-plan)
+    // (on the planner's stream, so the copies are ordered with its kernels)
     std::vector<WorldState> ws(p->W);
-    HIPCK(hipMemcpy(ws.data(), d.ws, sizeof(WorldState) * p->W, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpyAsync(ws.data(), d.ws, sizeof(WorldState) * p->W, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipStreamSynchronize(p->stream));
     for (int i = 0; i < p->W; i++) {
         for (int j = 0; j < NF; j++) ws[i].x[j] = x[j];
         ws[i].status = 0;
         ws[i].cur = 0;
     }
-    HIPCK(hipMemcpy(d.ws, ws.data(), sizeof(WorldState) * p->W, hipMemcpyHostToDevice));
+    HIPCK(hipMemcpyAsync(d.ws, ws.data(), sizeof(WorldState) * p->W, hipMemcpyHostToDevice, p->stream));
     launch_eval(p, dim3(p->T, p->W), 0);
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(g, d.g + gidx(d, 0, w, 0), sizeof(double) * d.m, hipMemcpyDeviceToHost, p->stream));
@@ -681,7 +745,26 @@ int armour_get_reach_dump(armour_planner* p, double* dump, int capacity) {
     return p->nops;
 }
 
+int armour_get_reach_occupancy(armour_planner* p, long long* used, long long* caps, int n) {
+    DeviceScope device_scope(p);
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
+    if (!p->lane_engine || !p->d_occ) return fail(ARMOUR_E_STATE, "occupancy is recorded by the bundle engine only");
+    unsigned long long o[8] = {0};
+    HIPCK(hipMemcpy(o, p->d_occ, sizeof(o), hipMemcpyDeviceToHost));
+    const long long u[ARMOUR_OCC_COUNT] = {(long long)o[0], (long long)o[1], (long long)o[2], (long long)o[3],
+                                           (long long)o[4], p->last_retried, p->last_failed};
+    const long long c[ARMOUR_OCC_COUNT] = {p->la.hcap, p->la.ccap, std::min<long long>(p->la.gcap, (1 << 16) - 1),
+                                           CAP_LM, CAP_UM, p->W, p->W};
+    for (int k = 0; k < n && k < ARMOUR_OCC_COUNT; k++) {
+        if (used) used[k] = u[k];
+        if (caps) caps[k] = c[k];
+    }
+    return ARMOUR_OCC_COUNT;
+}
+
 int armour_get_reach_program(const armour_planner* p, int* codes, int capacity) {
+    DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (codes && capacity >= p->nops) {
         std::vector<Op> ops(p->nops);

@@ -54,11 +54,14 @@ typedef struct armour_world {
 typedef struct armour_result {
     double k_opt[ARMOUR_NUM_FACTORS]; /* normalised, in [-1, 1] (MATLAB scales by pi/48) */
     int feasible;        /* finalize_solution re-check (KPR/NLPclass.cu:449-538) */
-    int solver_status;   /* 0 converged, 1 iteration cap, 2 line-search failure */
+    int solver_status;   /* 0 converged, 1 iteration cap, 2 line-search failure, 3 not planned (see error) */
     int iterations;
     int evaluations;
     double cost;         /* objective / COST_FUNCTION_OPTIMALITY_SCALE at k_opt */
     double kkt_error;
+    int error;           /* 0, or ARMOUR_E_CAPACITY: this world's reach set exceeded a capacity even
+                            after the retry with 4x buffers; it is reported infeasible and not planned,
+                            the other worlds of the batch are (armour_plan_batch still returns 0) */
 } armour_result;
 
 /* timings of the last batch, device-side (hipEvents on the planner's stream), milliseconds */
@@ -143,6 +146,13 @@ int armour_get_joint_bounds(const armour_planner* p, double* bounds28);
  * ARMOUR_PROFILE_OPS was set at armour_create, followed by 16 phase counters of the operator
  * paths (capacity counts pairs: >= op count + 8), and returns the op count. */
 int armour_get_reach_program(const armour_planner* p, int* codes, int capacity);
+/* Capacity headroom of the last reach (bundle engine): for k < n writes the largest use over the
+ * batch and its capacity: [0] arena union hashes, [1] arena coefficient rows, [2] terms of one
+ * operator (sort keys), [3] k-only monomials of a link PZ (reduce_link_PZ output), [4] k-only
+ * monomials of a torque PZ, [5] worlds retried with 4x buffers (cap: W), [6] worlds that still
+ * failed (cap: W). Returns ARMOUR_OCC_COUNT. */
+#define ARMOUR_OCC_COUNT 7
+int armour_get_reach_occupancy(armour_planner* p, long long* used, long long* caps, int n);
 int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms, int capacity);
 /* op-by-op state of job 0 (world 0, t = 0) of the last reach: per op 8 doubles [monomial count,
  * block size, centre[0..2], nominal ind[0], interval ind[0], sum|m|[0]] of the op's output, when

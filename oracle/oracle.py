@@ -36,6 +36,7 @@ def lib():
         L.oracle_reach.restype = ctypes.c_double
         L.oracle_reach.argtypes = [ctypes.c_void_p]
         L.oracle_num_constraints.argtypes = [ctypes.c_void_p]
+        L.oracle_set_obstacles.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp]
         L.oracle_bounds.argtypes = [ctypes.c_void_p, _dp, _dp]
         L.oracle_eval.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp]
         L.oracle_cost.restype = ctypes.c_double
@@ -83,6 +84,16 @@ class OraclePlanner:
         if self.reach_ms < 0:
             raise RuntimeError("oracle reach failed")
         return self.reach_ms
+
+    def set_obstacles(self, obstacles):
+        """replace the obstacle set after reach() (the reach sets do not depend on it; only the
+        buffered-obstacle hyperplanes are recomputed) — fixture tooling"""
+        obstacles = np.ascontiguousarray(np.asarray(obstacles, dtype=np.float64).reshape(-1, 12))
+        self.O = obstacles.shape[0]
+        self._obs = obstacles if self.O > 0 else np.zeros((1, 12))
+        if lib().oracle_set_obstacles(self.h, self.O, _ptr(self._obs)) != 0:
+            raise ValueError("oracle_set_obstacles failed")
+        self.m = lib().oracle_num_constraints(self.h)
 
     def bounds(self):
         gl = np.zeros(self.m)

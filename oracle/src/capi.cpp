@@ -138,6 +138,16 @@ double oracle_reach(void* h) {
     return std::chrono::duration<double, std::milli>(t1 - t0).count();
 }
 
+// test tooling: replace the obstacles after oracle_reach (hyperplanes only; 0 / -1)
+int oracle_set_obstacles(void* h, int O, const double* obstacles) {
+    try {
+        static_cast<Planner*>(h)->set_obstacles(O, obstacles);
+    } catch (...) {
+        return -1;
+    }
+    return 0;
+}
+
 int oracle_num_constraints(void* h) { return static_cast<Planner*>(h)->m(); }
 
 void oracle_bounds(void* h, double* gl, double* gu) { static_cast<Planner*>(h)->bounds(gl, gu); }

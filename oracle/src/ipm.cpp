@@ -245,6 +245,9 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             if (ls + 1 < opt.max_ls) alpha *= 0.5;
         }
         if (accepted && !ftype) { filt_theta.push_back((1 - 1e-5) * theta0); filt_phi.push_back(phi0 - 1e-8 * theta0); }
+        // a trial forced after max_ls halvings counts as a failed line search; three in a row end
+        // the solve (the role of Ipopt's failed restoration phase, which this solver does not have)
+        nfail = accepted ? 0 : nfail + 1;
         // 6. accept the trial point; multipliers with kappa_sigma safeguard
         double wa_new[NMAX] = {0};
         for (int r = 0; r < R; r++) {

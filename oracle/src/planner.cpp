@@ -61,7 +61,12 @@ void Planner::reach() {
         for (int i = 0; i < NF; i++) torque_radius[t * NF + i] += robot.friction[i];
     }
 
-    // CollisionChecking.cu:26-39 pair tables; :136-228 buffer + polytope_PH as CPU loops
+    buffer_obstacles();
+}
+
+// CollisionChecking.cu:26-39 pair tables; :136-228 buffer + polytope_PH as CPU loops. Depends on
+// the link generators of reach() and the obstacles only, so set_obstacles() can rerun it alone.
+void Planner::buffer_obstacles() {
     int combA[COMB], combB[COMB];
     {
         int a = 0, b = 1;
@@ -106,6 +111,13 @@ void Planner::reach() {
             }
         }
     }
+}
+
+void Planner::set_obstacles(int num_obstacles, const double* obs) {
+    if (num_obstacles < 0 || num_obstacles > MAX_OBS) throw std::runtime_error("Number of obstacles out of range");
+    O = num_obstacles;
+    obstacles.assign(obs, obs + O * (OBS_GEN + 1) * 3);
+    if (!link_gens.empty()) buffer_obstacles();
 }
 
 // NLPclass.cu:87-165

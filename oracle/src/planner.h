@@ -31,6 +31,9 @@ struct Planner {
     ~Planner();
 
     void reach();                     // armour_main.cu:97-222
+    void buffer_obstacles();          // CollisionChecking.cu:136-228 (part of reach())
+    // test tooling: replace the obstacle set after reach() (the reach sets do not depend on it)
+    void set_obstacles(int num_obstacles, const double* obs);
     int m() const { return NF * T + NJ * T * O + NF * 4; }  // NLPclass.cu:47-49
     void bounds(double* g_l, double* g_u) const;              // NLPclass.cu:87-165
     double eval_f(const double* x) const;                     // :207-236

@@ -1,0 +1,97 @@
+"""Generate the decision-boundary fixtures tests/golden/boundary_*.npz (build container, repo root):
+
+    python tests/golden/make_boundary.py
+
+Worlds come from tests/boundary_worlds.py (obstacles tuned with the oracle onto the collision
+threshold, start-collision worlds, torque-infeasible start states). Each fixture freezes the
+inputs and the oracle's (CPU restatement's) results on them: the collision decisions at the tuning
+point x0 (packed bits), the number of collision rows within 1e-3 of the 1e-4 threshold at x0 and
+at k_opt, and the plan (feasible, status, iterations, k_opt, cost). tests/test_boundary.py checks
+the oracle still reproduces them; tests/test_gpu_boundary.py checks the HIP path against a fresh
+oracle on the same worlds. Parity with the reference itself stays unpinned.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "armour-dev_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import boundary_worlds as B  # noqa: E402
+from oracle import OraclePlanner  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+PATTERN = ["graze", "graze", "graze_moving", "graze_moving", "graze", "torque", "start", "graze"]
+
+# name -> (T, O, number of worlds, kinds, tuned obstacles per graze world (None: half))
+SETS = {
+    "boundary_small_T20_O6": (20, 6, 12, PATTERN, None),
+    "boundary_config2_T100_O20": (100, 20, 16, PATTERN, None),
+    "boundary_config3_T200_O40": (200, 40, 6, ["graze", "graze_moving", "start", "torque", "graze", "graze"], 8),
+}
+
+
+def make_set(name, T, O, n, kinds, tuned):
+    rec = {k: [] for k in ("kinds", "q0", "qd0", "qdd0", "q_des", "obstacles", "x0", "feasible", "status",
+                           "iterations", "k_opt", "cost", "near_x0", "near_kopt", "dec_x0", "feasible_x0")}
+    for s in range(n):
+        kind = kinds[s % len(kinds)]
+        world, x0 = B.boundary_world(s, kind, T, O, n_tuned=tuned if kind.startswith("graze") else None)
+        R = OraclePlanner(*world, T=T, threads=8)
+        R.reach()
+        NJ = R.NJ
+        g0 = R.eval(x0, jac=False)
+        r = R.plan()
+        gk = R.eval(r["k_opt"], jac=False)
+        col = g0[B.collision_slice(T, NJ, O)]
+        for k, v in zip(("q0", "qd0", "qdd0", "q_des", "obstacles"), world):
+            rec[k].append(np.asarray(v, dtype=np.float64))
+        rec["kinds"].append(kind)
+        rec["x0"].append(x0)
+        rec["feasible"].append(r["feasible"])
+        rec["status"].append(r["status"])
+        rec["iterations"].append(r["iterations"])
+        rec["k_opt"].append(r["k_opt"])
+        rec["cost"].append(r["cost"])
+        rec["near_x0"].append(B.near_threshold_rows(g0, T, NJ, O))
+        rec["near_kopt"].append(B.near_threshold_rows(gk, T, NJ, O))
+        rec["dec_x0"].append(np.packbits(col > B.COL_THR))
+        rec["feasible_x0"].append(R.feasible(g0))
+        print(f"{name} {s:2d} {kind:13s} feasible={r['feasible']!s:5} status={r['status']} it={r['iterations']:3d} "
+              f"near@x0={rec['near_x0'][-1]:4d} near@kopt={rec['near_kopt'][-1]:4d}", flush=True)
+    out = {k: np.array(v) for k, v in rec.items()}
+    out["T"] = np.int64(T)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    return out
+
+
+def main():
+    summary = {}
+    only = sys.argv[1:]
+    for name, (T, O, n, kinds, tuned) in SETS.items():
+        if only and name not in only:
+            continue
+        t0 = time.time()
+        out = make_set(name, T, O, n, kinds, tuned)
+        summary[name] = dict(T=T, O=O, worlds=n, infeasible=int((~out["feasible"]).sum()),
+                             near_threshold_rows_x0=int(out["near_x0"].sum()),
+                             near_threshold_rows_kopt=int(out["near_kopt"].sum()),
+                             seconds=round(time.time() - t0, 1))
+    index = os.path.join(OUT, "boundary_index.json")
+    if os.path.exists(index):
+        summary = {**json.load(open(index))["sets"], **summary}
+    json.dump(dict(sets=summary, generator="tests/golden/make_boundary.py",
+                   oracle="oracle/ (CPU restatement); parity with the reference unpinned"),
+              open(os.path.join(OUT, "boundary_index.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+"""Decision-boundary fixtures (tests/golden/boundary_*.npz, made by tests/golden/make_boundary.py):
+the oracle reproduces its frozen decisions and plans, and the fixtures really sit on the
+reference's decisions — collision rows within 1e-3 of the 1e-4 threshold
+(KPR/NLPclass.cu:472-484), infeasible worlds (torque, collision, start-in-collision), the -1 path."""
+import os
+
+import numpy as np
+import pytest
+
+import boundary_worlds as B
+from oracle import OraclePlanner
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLD, name + ".npz")))
+
+
+def world(fx, w):
+    return fx["q0"][w], fx["qd0"][w], fx["qdd0"][w], fx["q_des"][w], fx["obstacles"][w]
+
+
+def check_world(fx, w, threads=4):
+    T = int(fx["T"])
+    O = fx["obstacles"].shape[1]
+    R = OraclePlanner(*world(fx, w), T=T, threads=threads)
+    R.reach()
+    g0 = R.eval(fx["x0"][w], jac=False)
+    col = g0[B.collision_slice(T, R.NJ, O)]
+    np.testing.assert_array_equal(np.packbits(col > B.COL_THR), fx["dec_x0"][w])
+    assert B.near_threshold_rows(g0, T, R.NJ, O) == fx["near_x0"][w]
+    assert R.feasible(g0) == bool(fx["feasible_x0"][w])
+    r = R.plan()
+    assert r["feasible"] == bool(fx["feasible"][w]) and r["status"] == fx["status"][w]
+    assert r["iterations"] == fx["iterations"][w]
+    np.testing.assert_allclose(r["k_opt"], fx["k_opt"][w], rtol=0, atol=1e-10)
+
+
+@pytest.mark.parametrize("w", range(12))
+def test_small_set_reproduced(w):
+    check_world(load("boundary_small_T20_O6"), w)
+
+
+@pytest.mark.parametrize("w", [0, 5, 6])
+def test_config2_set_reproduced(w):
+    """one graze, one torque, one start world of the config-2 set (the rest run on the GPU box)"""
+    check_world(load("boundary_config2_T100_O20"), w, threads=8)
+
+
+@pytest.mark.parametrize("name", ["boundary_small_T20_O6", "boundary_config2_T100_O20", "boundary_config3_T200_O40"])
+def test_fixture_sits_on_the_decisions(name):
+    fx = load(name)
+    feas = fx["feasible"]
+    kinds = fx["kinds"]
+    assert (~feas).mean() >= 0.25, "at least a quarter of the worlds infeasible"
+    assert feas.any(), "and some feasible against active constraints"
+    assert not feas[kinds == "start"].any(), "a world starting in collision is never feasible"
+    if name != "boundary_small_T20_O6":
+        assert fx["near_x0"].sum() + fx["near_kopt"].sum() >= 1000
+    # graze worlds: some collision decisions at x0 are violations, most rows are clear
+    for w in np.where(kinds == "graze")[0]:
+        T, O = int(fx["T"]), fx["obstacles"].shape[1]
+        bits = np.unpackbits(fx["dec_x0"][w])[: 7 * T * O]
+        assert bits.mean() < 0.05
+
+
+def test_start_obstacle_encloses_a_link():
+    """the start-collision obstacle covers a link's bounding sphere at q0"""
+    from armour_amd.robots import KINOVA
+    from armour_amd.worlds import link_spheres
+
+    fx = load("boundary_small_T20_O6")
+    for w in np.where(fx["kinds"] == "start")[0]:
+        ob = fx["obstacles"][w][-1]
+        cs, rs = link_spheres(KINOVA, fx["q0"][w])
+        half = np.abs(ob[3:].reshape(3, 3)).sum(axis=0)
+        inside = np.all(np.abs(cs - ob[:3]) + rs[:, None] <= half + 1e-12, axis=1)
+        assert inside.any()

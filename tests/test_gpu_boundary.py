@@ -1,0 +1,106 @@
+"""HIP path on the decision boundary (tests/golden/boundary_*.npz, see tests/boundary_worlds.py):
+worlds whose obstacles sit on the collision threshold, worlds starting in collision and worlds
+over the torque limits, against a fresh oracle on the same inputs.
+
+Bar (north_star): constraint values and Jacobian within 1e-9; every collision decision
+g > 1e-4 (KPR/NLPclass.cu:472-484) identical, counted on the rows within 1e-3 of the threshold;
+feasibility (finalize_solution, :422-538) identical; the solver's status and iteration count
+identical and k_opt within 1e-8 (1e-3 for an infeasible plan whose solve ended in line-search
+failure, see compare_set). The drop-in writes -1 for an infeasible world
+(KPR/armour_main.cu:326-334).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import armour_amd as A
+import boundary_worlds as B
+from oracle import OraclePlanner
+from test_boundary import load, world
+from test_gpu_drop_in import run, write_input
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+def compare_set(name, min_near):
+    fx = load(name)
+    T, W, O = int(fx["T"]), len(fx["kinds"]), fx["obstacles"].shape[1]
+    worlds = [world(fx, w) for w in range(W)]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    P.reach(worlds)
+    near = 0
+    refs = []
+    for w in range(W):
+        R = OraclePlanner(*worlds[w], T=T, threads=8)
+        R.reach()
+        refs.append(R)
+        np.testing.assert_allclose(P.torque_radius(w), R.torque_radius(), rtol=0, atol=TOL)
+        np.testing.assert_allclose(P.link_generators(w), R.link_gens(), rtol=0, atol=TOL)
+        for x in (fx["x0"][w], fx["k_opt"][w], 0.5 * (fx["x0"][w] + fx["k_opt"][w])):
+            g, J = P.eval_constraints(w, x)
+            go, Jo = R.eval(x)
+            np.testing.assert_allclose(g, go, rtol=0, atol=TOL)
+            np.testing.assert_allclose(J, Jo, rtol=0, atol=TOL)
+            cs = B.collision_slice(T, R.NJ, O)
+            np.testing.assert_array_equal(g[cs] > B.COL_THR, go[cs] > B.COL_THR)
+            assert R.feasible(g) == R.feasible(go)
+            near += B.near_threshold_rows(go, T, R.NJ, O)
+    assert near >= min_near, f"only {near} collision rows within 1e-3 of the threshold"
+    res, _ = P.plan(worlds)
+    infeasible = 0
+    for w, (r, R) in enumerate(zip(res, refs)):
+        ro = R.plan()
+        assert r["feasible"] == ro["feasible"], (w, fx["kinds"][w])
+        assert r["status"] == ro["status"] and r["iterations"] == ro["iterations"], (w, r["iterations"], ro["iterations"])
+        dk = float(np.abs(r["k_opt"] - ro["k_opt"]).max())
+        print(f"{name} world {w} ({fx['kinds'][w]}): feasible={r['feasible']} status={r['status']} "
+              f"iterations={r['iterations']} |dk_opt|={dk:.1e}")
+        # k_opt is the chosen parameter of a converged or feasible plan: 1e-8. A plan that ends in
+        # line-search failure and is infeasible writes -1 (k_opt unused). Its iterates run through
+        # nearly singular Newton systems (violated active constraints, z/s large), which amplify
+        # the ~1e-14 differences of g/J by up to ~1e3 per iteration
+        # (profiles/r02_ipm_divergence.log, tools/ipm_diverge.py: 5e-15 at iteration 1, 1e-8 at 7,
+        # 1e-4 at 16 for world 9 of the config-2 set). Such plans are held to identical status,
+        # iteration count and feasibility decision, and k_opt within 1e-3.
+        tol = 1e-8 if (r["status"] == 0 or r["feasible"]) else 1e-3
+        np.testing.assert_allclose(r["k_opt"], ro["k_opt"], rtol=0, atol=tol, err_msg=f"world {w}")
+        # and the frozen fixture (the oracle of the build container)
+        assert r["feasible"] == bool(fx["feasible"][w]) and r["iterations"] == fx["iterations"][w]
+        infeasible += not r["feasible"]
+    assert infeasible >= W / 4
+    return near, infeasible
+
+
+def test_boundary_small():
+    compare_set("boundary_small_T20_O6", 50)
+
+
+def test_boundary_config2():
+    """BASELINE configs[1] sizes (T=100, O=20) on the decision boundary"""
+    near, infeasible = compare_set("boundary_config2_T100_O20", 1000)
+    print(f"config 2 boundary: {near} near-threshold rows compared, {infeasible} infeasible plans")
+
+
+def test_boundary_config3():
+    """BASELINE configs[2] sizes (T=200, O=40) on the decision boundary"""
+    near, infeasible = compare_set("boundary_config3_T200_O40", 1000)
+    print(f"config 3 boundary: {near} near-threshold rows compared, {infeasible} infeasible plans")
+
+
+def test_drop_in_writes_minus_one_for_infeasible(tmp_path):
+    """armour_main on a start-in-collision world: armour.out is -1 then the time, exit 0
+    (KPR/armour_main.cu:326-334; MATLAB keeps its braking trajectory, uarmtd_planner.m:207-209)"""
+    fx = load("boundary_small_T20_O6")
+    w = int(np.where(fx["kinds"] == "start")[0][0])
+    write_input(str(tmp_path), world(fx, w))
+    r = run(str(tmp_path), int(fx["T"]))
+    assert r.returncode == 0, r.stderr
+    out = open(tmp_path / "armour.out").read().split()
+    assert len(out) == 2 and float(out[0]) == -1
+    # the planner's own verdict on the text-rounded inputs agrees
+    rounded = tuple(np.round(np.asarray(a, dtype=np.float64), 10) for a in world(fx, w))
+    P = A.Planner(T=int(fx["T"]), max_obstacles=fx["obstacles"].shape[1], max_worlds=1)
+    res, _ = P.plan([rounded])
+    assert not res[0]["feasible"]

@@ -21,8 +21,9 @@ COL_THR = 1e-4  # COLLISION_AVOIDANCE_CONSTRAINT_VIOLATION_THRESHOLD (Parameters
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def collision_rows(T, O):
-    return slice(7 * T, 7 * T + 7 * T * O)
+def collision_rows(T, O, NJ):
+    """g[7T + (l*T + t)*O + o] for every link l < NJ (NLPclass.cu:290-296; Fetch has NJ = 8)"""
+    return slice(7 * T, 7 * T + NJ * T * O)
 
 
 @pytest.mark.parametrize("name", golden_names())
@@ -41,7 +42,7 @@ def test_fixture(name):
             g, J = P.eval_constraints(0, x)
             np.testing.assert_allclose(g, g0, rtol=0, atol=TOL)
             np.testing.assert_allclose(J, J0, rtol=0, atol=TOL)
-            cr = collision_rows(T, O)
+            cr = collision_rows(T, O, P.NJ)
             np.testing.assert_array_equal(g[cr] > COL_THR, g0[cr] > COL_THR)
             assert chk.feasible(g) == bool(f0)
     res, tm = P.plan([world])
@@ -71,7 +72,7 @@ def _compare_batch(T, O, seeds, xs, robot=None):
             go, Jo = R.eval(x)
             np.testing.assert_allclose(g, go, rtol=0, atol=TOL)
             np.testing.assert_allclose(J, Jo, rtol=0, atol=TOL)
-            cr = collision_rows(T, O)
+            cr = collision_rows(T, O, P.NJ)
             np.testing.assert_array_equal(g[cr] > COL_THR, go[cr] > COL_THR)
             assert R.feasible(g) == R.feasible(go)
     res, _ = P.plan(worlds)
@@ -132,5 +133,5 @@ def test_rerun_bitwise_and_batch_position_stable():
         assert res_a[w]["feasible"] == res_b[4 - w]["feasible"]
         assert res_a[w]["iterations"] == res_b[4 - w]["iterations"]
         assert np.abs(g_a[w] - g_b[w]).max() < TOL
-        rows = collision_rows(T, O)
+        rows = collision_rows(T, O, P.NJ)
         assert np.array_equal(g_a[w][rows] > COL_THR, g_b[w][rows] > COL_THR)
