@@ -80,6 +80,8 @@ def lib():
         L.armour_reach_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Timing)]
         L.armour_eval_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
         L.armour_get_reach_program.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        L.armour_get_monomial_counts.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                                 ctypes.POINTER(ctypes.c_int)]
         L.armour_get_reach_occupancy.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
                                                  ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.armour_get_joint_bounds.argtypes = [ctypes.c_void_p, _dp]
@@ -97,7 +99,7 @@ ABI_SYMBOLS = ["armour_create", "armour_create_robot", "armour_robot_builtin", "
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
-               "armour_get_reach_dump", "armour_get_reach_occupancy"]
+               "armour_get_reach_dump", "armour_get_reach_occupancy", "armour_get_monomial_counts"]
 
 
 def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
@@ -241,6 +243,14 @@ class Planner:
         _check(min(0, lib().armour_get_reach_profile(self.h, buf, n + 8)))
         a = np.array(buf[:], dtype=np.uint64)
         return a[:2 * n].reshape(n, 2), a[2 * n:]
+
+    def monomial_counts(self, w):
+        """(link [T, NJ], torque [T, 7]) k-only monomial counts of world w"""
+        lk = np.zeros((self.T, self.NJ), dtype=np.int32)
+        tq = np.zeros((self.T, NF), dtype=np.int32)
+        _check(lib().armour_get_monomial_counts(self.h, w, lk.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                                tq.ctypes.data_as(ctypes.POINTER(ctypes.c_int))))
+        return lk, tq
 
     OCCUPANCY = ("arena_hashes", "arena_rows", "operator_terms", "link_monomials", "torque_monomials",
                  "worlds_retried", "worlds_failed")

@@ -38,17 +38,24 @@ def best(allrec: np.ndarray) -> int:
     return int(np.argmin(np.where(feas, allrec[:, 7], np.inf)))
 
 
-def gather(rec: np.ndarray, dist=None, device=None):
-    """All-gather equal-sized record blocks from every rank; returns (all records, best index).
-    `dist` is torch.distributed (initialised) or None for a single process."""
+def gather(rec: np.ndarray, dist=None, device=None, total=None):
+    """All-gather the record blocks of every rank; returns (all records in world order, best index).
+    `dist` is torch.distributed (initialised) or None for a single process. With `total` (the job's
+    world count, sharded by shard()) the blocks may differ by one row: each is padded to the largest
+    for the collective and trimmed after."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return rec, best(rec)
     import torch
 
-    t = torch.from_numpy(np.ascontiguousarray(rec))
+    ws = dist.get_world_size()
+    sizes = [len(shard(total, r, ws)) for r in range(ws)] if total is not None else [len(rec)] * ws
+    rows = max(sizes)
+    padded = np.zeros((rows, RECORD))
+    padded[:len(rec)] = rec
+    t = torch.from_numpy(padded)
     if device is not None:
         t = t.to(device)
-    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    out = [torch.empty_like(t) for _ in range(ws)]
     dist.all_gather(out, t)
-    allrec = torch.cat(out).cpu().numpy()
+    allrec = np.concatenate([o.cpu().numpy()[:n] for o, n in zip(out, sizes)])
     return allrec, best(allrec)

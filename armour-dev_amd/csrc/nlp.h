@@ -39,6 +39,7 @@ struct WorldState {
     int accepted_ok;   // last acceptance passed the filter (0: forced after max_ls trials)
     int ftype;
     int first_update, nfail, iter, nevals, ls;
+    int spec_k;        // trial of the speculative round that ended the line search (-1: none)
 };
 
 struct NlpDev {
@@ -68,8 +69,30 @@ struct NlpDev {
     double *slo, *shi, *zlo, *zhi, *dslo, *dshi, *dzlo, *dzhi, *rplo, *rphi;
     double* partial;        // [W][nblk][KA]
     WorldState* ws;         // [W]
-    int* flags;             // [0]: any world still searching, [1]: any world running
+    int* flags;             // mapped host memory: [0] worlds running (round 0 of an iteration),
+                            // [1] worlds still searching after the last line-search round
+    // Active-world compaction: a solver launch covers only the worlds of list `wl` (blockIdx -> wl[b];
+    // null: every world, blockIdx = world). ipm_world_C appends the worlds still running (round 0)
+    // and still searching into wl_run / wl_search; the last block publishes the counts to flags.
+    const int* wl;
+    int* wl_run;
+    int* wl_search;
+    unsigned* cnt;          // device: [0] running, [1] searching, [2] block ticket
+    int ls0;                // this ipm_world_C launch is round 0 of an iteration
+    // rounds launched without a host synchronisation: grids sized by an upper bound, the list's
+    // true length in device memory (lcount; null: the grid is exact); ipm_world_C stores the length
+    // of the list it appends to into lcount_out
+    const unsigned* lcount;
+    unsigned* lcount_out;
+    // Speculative line-search round: the remaining K = max_ls - 1 trial points of up to NSPEC
+    // searching worlds evaluated at once into their own slots, [list entry i][trial k] (see
+    // ipm_world_Cs); the trial that ends the search is copied into the world's trial slot.
+    int K;
+    double *gs, *Js, *fs, *grads, *lcs_s, *partial_s;
 };
+constexpr int NSPEC = 16;
+
+AD int world_of(const NlpDev& d, int b) { return d.wl ? d.wl[b] : b; }
 
 AD long gidx(const NlpDev& d, int slot, int w, long r) { return ((long)slot * d.W + w) * d.m + r; }
 

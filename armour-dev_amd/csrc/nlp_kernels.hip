@@ -228,10 +228,18 @@ __device__ double wrap_to_pi(double a) {
 // copies the current slot's, the final iterate's, out).
 template <typename R>
 __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
-    const int t = blockIdx.x, w = blockIdx.y;
+    // mode 3: speculative trial k of list entry i (blockIdx.y = i * K + k) into its own slot
+    if (mode == 1 && d.lcount && blockIdx.y >= *d.lcount) return;
+    const int t = blockIdx.x, w = mode == 3 ? d.wl[blockIdx.y / d.K] : world_of(d, blockIdx.y);
     WorldState& S = d.ws[w];
-    if (mode == 1 && !(S.status == 0 && S.searching)) return;
+    if (mode >= 1 && !(S.status == 0 && S.searching)) return;
     const int slot = mode == 0 ? 0 : 1 - S.cur;
+    double* const Gb = mode == 3 ? d.gs + (long)blockIdx.y * d.m : d.g + gidx(d, slot, w, 0);
+    double* const Jb = mode == 3 ? d.Js + (long)blockIdx.y * d.m * NF : d.J + gidx(d, slot, w, 0) * NF;
+    double* const Lcb = mode == 3 ? d.lcs_s + (long)blockIdx.y * d.T * d.NJ * 3
+                                  : d.link_c + slot * d.lcs + (long)w * d.T * d.NJ * 3;
+    double* const fb = mode == 3 ? d.fs + blockIdx.y : d.f + slot * d.W + w;
+    double* const gradb = mode == 3 ? d.grads + (long)blockIdx.y * NF : d.grad + ((long)slot * d.W + w) * NF;
     const RobotParams& rp = *d.rp;
     const int tid = threadIdx.x;
     const long jt = (long)w * d.T + t;
@@ -259,7 +267,12 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     __shared__ int lcnt[MAX_J], tcnt[NF];
     __shared__ R ptab[NF][8];
     if (tid < NF) {
-        const double xd = mode == 1 ? S.xt[tid] : S.x[tid];
+        double xd = mode == 1 ? S.xt[tid] : S.x[tid];
+        if (mode == 3) {  // alpha halved k times and x + alpha dx: ipm_world_C's arithmetic
+            double a = S.alpha;
+            for (int k = 0; k < (int)(blockIdx.y % d.K); k++) a *= 0.5;
+            xd = S.x[tid] + a * S.dx[tid];
+        }
         x[tid] = xd;
         const R xj = (R)xd;
         ptab[tid][0] = (R)1.0; ptab[tid][1] = xj; ptab[tid][2] = xj * xj; ptab[tid][3] = xj * xj * xj;
@@ -326,7 +339,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
             const R r = d.ro.link_rad[base * 3 + e];
             const R cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
             lc[l][e] = cc;
-            d.link_c[slot * d.lcs + base * 3 + e] = cc;
+            Lcb[((long)t * NJ + l) * 3 + e] = cc;
         } else {
             dlc[l][k - 1][e] = c;
         }
@@ -338,12 +351,12 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         R c = k == 0 ? d.ro.tq_center[base] : 0.0;
         const int cnt = tcnt[j];
         for (int q = 0; q < cnt; q++) c = c + slice_term(tco[j][q], th[j][q], k, ptab);
-        const long gi = gidx(d, slot, w, (long)t * NF + j);
+        const long gi = (long)t * NF + j;
         if (k == 0) {
             const R r = d.ro.tq_rad[base];
-            d.g[gi] = ((c - r) + (c + r)) * 0.5;
+            Gb[gi] = ((c - r) + (c + r)) * 0.5;
         } else {
-            d.J[gi * NF + k - 1] = c;
+            Jb[gi * NF + k - 1] = c;
         }
       }
     }
@@ -363,15 +376,15 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
                 extremum(kind, q0[i], Tq, TTq, ka, &mn, &mx, &mnid, &mxid, &e2, &e3);
                 const double scale = kind == 0 ? 1.0 : D;
                 const long rmin = off2 + kind * 2 * NF + i, rmax = rmin + NF;
-                const long gmin = gidx(d, slot, w, rmin), gmax = gidx(d, slot, w, rmax);
-                d.g[gmin] = mn / scale;
-                d.g[gmax] = mx / scale;
+                const long gmin = rmin, gmax = rmax;
+                Gb[gmin] = mn / scale;
+                Gb[gmax] = mx / scale;
                 const double gmn = extremum_grad(kind, mnid, e2, e3) * rp.k_range[i] / scale;
                 const double gmx = extremum_grad(kind, mxid, e2, e3) * rp.k_range[i] / scale;
 #pragma unroll
                 for (int k = 0; k < NF; k++) {
-                    d.J[gmin * NF + k] = (k == i) ? gmn : 0.0;
-                    d.J[gmax * NF + k] = (k == i) ? gmx : 0.0;
+                    Jb[gmin * NF + k] = (k == i) ? gmn : 0.0;
+                    Jb[gmax * NF + k] = (k == i) ? gmx : 0.0;
                 }
             }
         // cost: wrapped joints summed first (NLPclass.cu:225-233)
@@ -388,11 +401,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
                 fv = first ? term : fv + term;
                 first = false;
             }
-        d.f[slot * d.W + w] = fv * rp.cost_scale;
+        *fb = fv * rp.cost_scale;
         for (int i = 0; i < NF; i++) {
             const double dk = tp * tp * tp * (6 * tp * tp - 15 * tp + 10) * rp.k_range[i];
             double gv = rp.wrap_mask[i] ? (2 * wrap_to_pi(qp[i] - d.qdes[w * NF + i]) * dk) : (2 * (qp[i] - d.qdes[w * NF + i]) * dk);
-            d.grad[((long)slot * d.W + w) * NF + i] = gv * rp.cost_scale;
+            gradb[i] = gv * rp.cost_scale;
         }
     }
     __syncthreads();
@@ -549,12 +562,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
             }
         if (mwin >= 0) plane_normal(obs[o] + 3 * (mwin / 6 + 1), lgen[l] + 3 * (mwin % 6), B0, B1, B2);
         const long row = nt + ((long)l * d.T + t) * O + o;
-        const long gi = gidx(d, slot, w, row);
-        d.g[gi] = -best;
+        Gb[row] = -best;
 #pragma unroll
         for (int k = 0; k < NF; k++) {
             const R dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
-            d.J[gi * NF + k] = isneg ? dot : -dot;
+            Jb[row * NF + k] = isneg ? dot : -dot;
         }
     }
 }
@@ -585,6 +597,8 @@ __global__ void ipm_world_init(NlpDev d) {
     S.nfilt = 0;
     S.cur = 0;
     S.status = d.ro.err[w] ? 4 : 0;  // 4: reach set over capacity (planner.hip run_reach), not planned
+    d.wl_run[w] = w;                 // the first iteration covers every world
+    if (w == 0) { d.cnt[0] = 0; d.cnt[1] = 0; d.cnt[2] = 0; }
     S.searching = 0;
     S.first_update = 1;
     S.nfail = 0;
@@ -621,7 +635,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
 
 // pass A: residuals, errors, reduced Newton system sums
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
-    const int w = blockIdx.y;
+    const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
     __shared__ double lds[(ROW_THREADS / 64) * 53];
@@ -722,7 +736,15 @@ __device__ bool chol_solve7(const double* M, double shift, const double* b, doub
 // onto init. The per-world kernels run one wave per world: the nblk dependent load rounds of a
 // single thread become one round per lane.
 template <int N>
+__device__ inline void world_partials_at(const double* base, int nblk, const double (&init)[N], const int (&op)[N],
+                                         double (&P)[N]);
+template <int N>
 __device__ inline void world_partials(const NlpDev& d, int w, const double (&init)[N], const int (&op)[N], double (&P)[N]) {
+    world_partials_at(d.partial + (long)w * d.nblk * KA, d.nblk, init, op, P);
+}
+template <int N>
+__device__ inline void world_partials_at(const double* base, int nblk, const double (&init)[N], const int (&op)[N],
+                                         double (&P)[N]) {
     const int lane = threadIdx.x & 63;
     double s = 0;
     int o = 0;
@@ -730,8 +752,8 @@ __device__ inline void world_partials(const NlpDev& d, int w, const double (&ini
     for (int q = 0; q < N; q++)
         if (q == lane) { s = init[q]; o = op[q]; }
     if (lane < N) {
-        const double* in = d.partial + (long)w * d.nblk * KA + lane;
-        for (int b = 0; b < d.nblk; b++) {
+        const double* in = base + lane;
+        for (int b = 0; b < nblk; b++) {
             const double x = in[(long)b * KA];
             s = o == 0 ? s + x : o == 1 ? fmax(s, x) : fmin(s, x);
         }
@@ -746,7 +768,7 @@ __device__ inline void world_partials(const NlpDev& d, int w, const double (&ini
 }
 
 __global__ void ipm_world_A(NlpDev d, int nside) {
-    const int w = blockIdx.x;
+    const int w = world_of(d, blockIdx.x);
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
     if (S.iter >= d.opt.max_iter) {  // oracle: loop ends without a final check
@@ -795,7 +817,7 @@ __global__ void ipm_world_A(NlpDev d, int nside) {
 
 // pass B: step components, fraction to boundary, line-search ingredients
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
-    const int w = blockIdx.y;
+    const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
     __shared__ double lds[(ROW_THREADS / 64) * 53];
@@ -849,7 +871,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
 }
 
 __global__ void ipm_world_B(NlpDev d) {
-    const int w = blockIdx.x;
+    const int w = world_of(d, blockIdx.x);
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
     double P[19], init[19];
@@ -880,7 +902,8 @@ __global__ void ipm_world_B(NlpDev d) {
 
 // pass C: barrier objective and constraint violation at the trial point
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
-    const int w = blockIdx.y;
+    if (d.lcount && blockIdx.y >= *d.lcount) return;
+    const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
     __shared__ double lds[(ROW_THREADS / 64) * 53];
@@ -900,8 +923,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
     block_reduce_n(v, kinds, lds, out);
 }
 
-__global__ void ipm_world_C(NlpDev d) {
-    const int w = blockIdx.x;
+__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft);
+__device__ inline void world_C_body(const NlpDev& d, int w) {
     WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
     double P[2];
@@ -909,9 +932,13 @@ __global__ void ipm_world_C(NlpDev d) {
     const int op[2] = {0, 0};
     world_partials(d, w, init, op, P);
     if (threadIdx.x != 0) return;
-    const double logt = P[0], rpt = P[1];
+    accept_trial(d, S, P[0], P[1], d.f[(1 - S.cur) * d.W + w]);
+}
+
+// the filter acceptance test of one trial point (barrier terms logt, violation rpt, objective ft);
+// on failure the next trial (alpha halved) or, after max_ls trials, the forced last one
+__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft) {
     S.nevals++;
-    const double ft = d.f[(1 - S.cur) * d.W + w];
     const double phit = ft - S.mu * logt, thetat = rpt;
     bool ok = thetat <= S.theta_max;
     for (int q = 0; ok && q < S.nfilt; q++)
@@ -945,12 +972,116 @@ __global__ void ipm_world_C(NlpDev d) {
     }
     S.alpha *= 0.5;
     for (int j = 0; j < NF; j++) S.xt[j] = S.x[j] + S.alpha * S.dx[j];
-    d.flags[0] = 1;  // mapped host memory: a plain store, every writer stores 1
+}
+
+// one line-search round's acceptance test per world, then the compaction bookkeeping: the worlds
+// still running (round 0) and still searching are appended to the next lists (their order only
+// decides which block serves which world), and the last block to finish publishes both counts to
+// the mapped host flags and resets the counters for the next launch.
+__global__ void ipm_world_C(NlpDev d) {
+    const bool valid = !d.lcount || blockIdx.x < *d.lcount;
+    const int w = valid ? world_of(d, blockIdx.x) : 0;
+    if (valid) world_C_body(d, w);
+    if (threadIdx.x != 0) return;
+    const WorldState& S = d.ws[w];
+    if (valid && S.status == 0) {
+        if (d.ls0) d.wl_run[atomicAdd(&d.cnt[0], 1u)] = w;
+        if (S.searching) d.wl_search[atomicAdd(&d.cnt[1], 1u)] = w;
+    }
+    __threadfence();
+    if (atomicAdd(&d.cnt[2], 1u) == gridDim.x - 1) {
+        __threadfence();
+        const unsigned nrun = atomicAdd(&d.cnt[0], 0u), nsearch = atomicAdd(&d.cnt[1], 0u);
+        if (d.ls0) d.flags[0] = (int)nrun;
+        d.flags[1] = (int)nsearch;
+        if (d.lcount_out) *d.lcount_out = nsearch;
+        d.cnt[0] = 0;
+        d.cnt[1] = 0;
+        d.cnt[2] = 0;
+    }
+}
+
+// Speculative line-search round (the tail: few worlds still searching after round 0). Pass C of
+// every remaining trial k = 0 .. K-1 (alpha halved k times) of list entry i, blockIdx.y = i * K + k,
+// from the trial's own slot; the arithmetic of ipm_rows_C at that trial.
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
+    const int i = blockIdx.y / d.K, k = blockIdx.y % d.K;
+    const int w = d.wl[i];
+    const WorldState& S = d.ws[w];
+    if (!(S.status == 0 && S.searching)) return;
+    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    double alpha = S.alpha, xt[NF];
+    for (int q = 0; q < k; q++) alpha *= 0.5;
+#pragma unroll
+    for (int j = 0; j < NF; j++) xt[j] = S.x[j] + alpha * S.dx[j];
+    const double* G = d.gs + (long)blockIdx.y * d.m;
+    double logt = 0, rpt = 0;
+    const long r0 = (long)blockIdx.x * d.chunk;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        const double v = r < d.m ? G[r] : xt[r - d.m];
+        const long ii = (long)w * d.R + r;
+        const double L = d.L[ii], U = d.U[ii];
+        if (has_lo(d, L)) { const double st = d.slo[ii] + alpha * d.dslo[ii]; logt += log(st); rpt += fabs((v - L) - st); }
+        if (has_hi(d, U)) { const double st = d.shi[ii] + alpha * d.dshi[ii]; logt += log(st); rpt += fabs((U - v) - st); }
+    }
+    double* out = d.partial_s + ((long)blockIdx.y * d.nblk + blockIdx.x) * KA;
+    double v[2] = {logt, rpt};
+    const int kinds[2] = {0, 0};
+    block_reduce_n(v, kinds, lds, out);
+}
+
+// the trials of a speculative round tested in order, exactly as the sequential rounds would
+// (ipm_world_C): the first acceptable one ends the search, or the last (forced) one
+__global__ void ipm_world_Cs(NlpDev d) {
+    const int w = d.wl[blockIdx.x];
+    WorldState& S = d.ws[w];
+    int chosen = -1;
+    for (int k = 0; k < d.K; k++) {
+        int go = 0;
+        if (threadIdx.x == 0) go = S.status == 0 && S.searching;
+        if (!__shfl(go, 0)) break;
+        double P[2];
+        const double init[2] = {0.0, 0.0};
+        const int op[2] = {0, 0};
+        const long sidx = (long)blockIdx.x * d.K + k;
+        world_partials_at(d.partial_s + sidx * d.nblk * KA, d.nblk, init, op, P);
+        if (threadIdx.x == 0) {
+            accept_trial(d, S, P[0], P[1], d.fs[sidx]);
+            chosen = k;
+        }
+    }
+    if (threadIdx.x == 0) S.spec_k = chosen;
+}
+
+// the chosen trial's g, J, link centres, f and gradient into the world's trial slot
+__global__ void ipm_copy_spec(NlpDev d) {
+    const int w = d.wl[blockIdx.y];
+    const WorldState& S = d.ws[w];
+    if (S.spec_k < 0) return;
+    const long sidx = (long)blockIdx.y * d.K + S.spec_k;
+    const int slot = 1 - S.cur;
+    const long nlc = (long)d.T * d.NJ * 3, nj = (long)d.m * NF;
+    const long n = d.m + nj + nlc;
+    double* g = d.g + gidx(d, slot, w, 0);
+    double* J = d.J + gidx(d, slot, w, 0) * NF;
+    double* lc = d.link_c + slot * d.lcs + (long)w * nlc;
+    const double* gs = d.gs + sidx * d.m;
+    const double* Js = d.Js + sidx * nj;
+    const double* ls = d.lcs_s + sidx * nlc;
+    for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
+        if (q < d.m) g[q] = gs[q];
+        else if (q < d.m + nj) J[q - d.m] = Js[q - d.m];
+        else lc[q - d.m - nj] = ls[q - d.m - nj];
+    }
+    if (blockIdx.x == 0 && threadIdx.x < NF) {
+        d.grad[((long)slot * d.W + w) * NF + threadIdx.x] = d.grads[sidx * NF + threadIdx.x];
+        if (threadIdx.x == 0) d.f[slot * d.W + w] = d.fs[sidx];
+    }
 }
 
 // pass D: accept the trial point — slacks, multipliers, BFGS ingredients
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
-    const int w = blockIdx.y;
+    const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
     __shared__ double lds[(ROW_THREADS / 64) * 53];
@@ -988,7 +1119,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
 }
 
 __global__ void ipm_world_D(NlpDev d) {
-    const int w = blockIdx.x;
+    const int w = world_of(d, blockIdx.x);
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
     double wn[NF];
@@ -1032,7 +1163,6 @@ __global__ void ipm_world_D(NlpDev d) {
     S.nfail = S.accepted_ok ? 0 : S.nfail + 1;
     S.iter++;
     if (S.nfail >= 3) S.status = 3;
-    if (S.status == 0) d.flags[1] = 1;
 }
 
 // finalize_solution's feasibility re-check (NLPclass.cu:449-538): one block per world

@@ -69,15 +69,19 @@ struct armour_planner {
     ReachOut ro;
     ReachArgs ra;
     // bundle engine (lane_kernel.hip): default; ARMOUR_ENGINE=job selects the per-job reach_kernel
-    bool lane_engine = true;
+    bool lane_engine = true;  // the last batch ran on the bundle engine
+    bool has_lane = false, has_job = false;  // engines with buffers
+    long job_max = 0;         // batches of at most this many jobs (W x T) run on the per-job engine
+    bool job_fits = true;     // the reach program's payload pool fits the per-job engine's LDS
     bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
     int lane_grid = 0;
     lane::LaneArgs la;
     // nlp
     NlpDev d;
     int* feas = nullptr;
-    int* flags = nullptr;     // device
-    int* h_flags = nullptr;   // pinned host
+    int* h_flags = nullptr;   // pinned host, mapped (NlpDev::flags)
+    int* d_lists = nullptr;   // [4][max_worlds] active-world lists of the solver
+    bool spec = true;         // speculative line-search rounds (ARMOUR_NO_SPEC: sequential only)
     WorldState* h_ws = nullptr;
     double* h_f = nullptr;
     int* h_feas = nullptr;
@@ -107,6 +111,9 @@ static int row_chunk() {
 
 // capacity retry: a quarter of the workgroups, each with four workgroups' buffers
 constexpr int RETRY_SCALE = 4;
+
+// largest batch (jobs = worlds x T) that runs on the per-job engine; measured crossover, DESIGN.md §4
+constexpr long JOB_ENGINE_JOBS = 3072;
 
 static int planner_init(armour_planner* p, const armour_config* cfg, const armour_robot* robot) {
     p->cfg = *cfg;
@@ -162,6 +169,9 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             const char* eng = std::getenv("ARMOUR_ENGINE");
             const bool job_engine = eng && std::strcmp(eng, "job") == 0;
             // the bundle engine's payload pool lives in HBM, sized below; the per-job engine's in LDS
+            // (POOL_DOUBLES): a robot whose program does not fit it (Fetch: 8 links) runs on the
+            // bundle engine only
+            p->job_fits = pool <= POOL_DOUBLES;
             if (pb.nslots > MAX_SLOTS || (job_engine && pool > POOL_DOUBLES)) {
                 char buf[200];
                 std::snprintf(buf, sizeof(buf), "reach program needs %d handle slots (kernel: %d) and %d payload doubles (per-job engine: %d)",
@@ -188,6 +198,21 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         const int per = wg ? std::atoi(wg) : REACH_WG_PER_CU;
         p->reach_grid = (per >= 1 && per <= REACH_WG_PER_CU ? per : REACH_WG_PER_CU) * p->ncu;
     }
+    // Engine choice per batch. The bundle engine (lane_kernel.hip) runs 64 jobs per workgroup and
+    // fills the chip from ~2 x CUs x 64 jobs on, but one bundle takes ~18 ms whatever its size. The
+    // per-job engine (reach_kernel.hip) runs one job per workgroup, ~4 ms per round of up to
+    // 4 x CUs jobs. So small batches (the drop-in's single plan) take the per-job engine:
+    // batches of at most job_max jobs (ARMOUR_JOB_ENGINE_JOBS; ARMOUR_ENGINE=job|lane forces one).
+    {
+        const char* eng = std::getenv("ARMOUR_ENGINE");
+        const char* jm = std::getenv("ARMOUR_JOB_ENGINE_JOBS");
+        p->job_max = jm ? std::atol(jm) : JOB_ENGINE_JOBS;
+        if (eng && std::strcmp(eng, "job") == 0) p->job_max = (long)Wm * T;
+        if ((eng && std::strcmp(eng, "lane") == 0) || !p->job_fits) p->job_max = 0;
+        p->has_job = p->job_max > 0;
+        p->has_lane = (long)Wm * T > p->job_max;
+        if (p->has_job) p->reach_grid = (int)std::min<long>(p->reach_grid, std::min<long>(p->job_max, (long)Wm * T));
+    }
     ReachArgs& ra = p->ra;
     ra.prog = p->d_prog;
     ra.nops = p->nops;
@@ -207,12 +232,10 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     }
     if ((rc = p->alloc(&p->d_jrs, jobs * NF))) return rc;
     {
-        const char* eng = std::getenv("ARMOUR_ENGINE");
-        p->lane_engine = !(eng && std::strcmp(eng, "job") == 0);
         const char* f32 = std::getenv("ARMOUR_EVAL_F32");
         p->eval_f32 = f32 && std::atoi(f32) != 0;
     }
-    if (!p->lane_engine) {
+    if (p->has_job) {
         ra.arena_cap = 1 << 17;
         ra.gcap = 1 << 15;
         if ((rc = p->alloc(&ra.arena_h, (size_t)p->reach_grid * ra.arena_cap)) ||
@@ -221,7 +244,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             (rc = p->alloc(&ra.gkp, (size_t)p->reach_grid * ra.gcap)) ||
             (rc = p->alloc(&ra.gout, (size_t)p->reach_grid * ra.gcap * 9)))
             return rc;
-    } else {
+    }
+    if (p->has_lane) {
         // one resident bundle workgroup per CU, each with its own arena; sizes from the measured
         // per-job use (~16.5k monomials) times the union inflation, with margin
         lane::LaneArgs& la = p->la;
@@ -266,6 +290,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             if ((rc = p->alloc(&p->d_dump, (size_t)p->nops * DUMP_W * lane::LG))) return rc;
             HIPCK(hipMemset(p->d_dump, 0, sizeof(double) * p->nops * DUMP_W * lane::LG));
             la.dump = p->d_dump;
+            ra.dump = nullptr;  // the op dump follows the bundle engine when it exists
         }
     }
     // NLP
@@ -294,6 +319,25 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // host clears and reads them between synchronised rounds (no fill or copy per round)
     HIPCK(hipHostMalloc((void**)&p->h_flags, 4 * sizeof(int), hipHostMallocMapped));
     HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
+    // active-world lists: two per iteration (ping-pong), two per line-search round
+    if ((rc = p->alloc(&p->d_lists, 4 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 8))) return rc;
+    // speculative line-search slots: NSPEC worlds x (max_ls - 1) trials
+    d.K = d.opt.max_ls - 1;
+    p->spec = !std::getenv("ARMOUR_NO_SPEC") && d.K > 0;
+    if (p->spec) {
+        const size_t ns = (size_t)std::min(Wm, NSPEC) * d.K;
+        if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.Js, ns * mmax * NF)) || (rc = p->alloc(&d.fs, ns)) ||
+            (rc = p->alloc(&d.grads, ns * NF)) || (rc = p->alloc(&d.lcs_s, ns * T * NJ * 3)) ||
+            (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
+            return rc;
+    }
+    HIPCK(hipMemset(d.cnt, 0, 8 * sizeof(unsigned)));
+    d.lcount = nullptr;
+    d.lcount_out = nullptr;
+    d.wl = nullptr;
+    d.wl_run = p->d_lists;
+    d.wl_search = p->d_lists + 2 * Wm;
+    d.ls0 = 0;
     HIPCK(hipHostMalloc((void**)&p->h_ws, Wm * sizeof(WorldState)));
     HIPCK(hipHostMalloc((void**)&p->h_f, 2 * Wm * sizeof(double)));
     HIPCK(hipHostMalloc((void**)&p->h_feas, Wm * sizeof(int)));
@@ -354,6 +398,7 @@ static int run_reach(armour_planner* p) {
     if (p->d_occ) HIPCK(hipMemsetAsync(p->d_occ, 0, sizeof(unsigned long long) * 8, p->stream));
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
+    p->lane_engine = !(p->has_job && jobs <= p->job_max);
     const long nj = jobs * NF;
     HIPCK(hipEventRecord(p->ev[3], p->stream));
     hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, p->stream, p->d_rp, p->W, p->T, p->q0, p->qd0,
@@ -448,39 +493,79 @@ static void launch_eval(armour_planner* p, dim3 grid, int mode) {
 static int run_solver(armour_planner* p) {
     NlpDev& d = p->d;
     const int W = p->W;
-    const dim3 rows(d.nblk, W), evg(p->T, W);
-    const int wb = (W + 63) / 64;
-    hipLaunchKernelGGL(ipm_world_init, dim3(wb), dim3(64), 0, p->stream, d);
-    launch_eval(p, evg, 0);
-    hipLaunchKernelGGL(ipm_rows_init, rows, dim3(ROW_THREADS), 0, p->stream, d);
+    int* Li[2] = {p->d_lists, p->d_lists + p->Wmax};                  // worlds of an iteration
+    int* Ls[2] = {p->d_lists + 2 * p->Wmax, p->d_lists + 3 * p->Wmax};  // worlds of a line-search round
+    d.wl = nullptr;
+    d.wl_run = Li[0];
+    d.ls0 = 0;
+    hipLaunchKernelGGL(ipm_world_init, dim3((W + 63) / 64), dim3(64), 0, p->stream, d);
+    launch_eval(p, dim3(p->T, W), 0);
+    hipLaunchKernelGGL(ipm_rows_init, dim3(d.nblk, W), dim3(ROW_THREADS), 0, p->stream, d);
     HIPCK(hipGetLastError());
     const int ns = nside_count(p);
-    // One host synchronisation per line-search round. world_D's "any world running" flag is read
-    // at the next iteration's first round: the kernels queued in between exit at once for worlds
-    // that are no longer running, so a finished batch only costs one round of empty launches.
-    bool done = false;
-    for (int it = 0; it <= d.opt.max_iter && !done; it++) {
-        hipLaunchKernelGGL(ipm_rows_A, rows, dim3(ROW_THREADS), 0, p->stream, d);
-        hipLaunchKernelGGL(ipm_world_A, dim3(W), dim3(64), 0, p->stream, d, ns);
-        hipLaunchKernelGGL(ipm_rows_B, rows, dim3(ROW_THREADS), 0, p->stream, d);
-        hipLaunchKernelGGL(ipm_world_B, dim3(W), dim3(64), 0, p->stream, d);
-        for (int ls = 0; ls < d.opt.max_ls; ls++) {
-            p->h_flags[0] = 0;  // no kernel in flight writes it (world_C's last round was synchronised)
-            launch_eval(p, evg, 1);
-            hipLaunchKernelGGL(ipm_rows_C, rows, dim3(ROW_THREADS), 0, p->stream, d);
-            hipLaunchKernelGGL(ipm_world_C, dim3(W), dim3(64), 0, p->stream, d);
+    // Launches cover the active worlds only (NlpDev::wl): every line-search round's ipm_world_C
+    // compacts the worlds still running / still searching into the next lists and publishes the
+    // counts in mapped host memory, read after the round's one host synchronisation. Inactive
+    // worlds in a list (finished by ipm_world_A / _D since) exit at once. A world's arithmetic does
+    // not depend on which block serves it, so the results are those of full launches.
+    int cur = 0, nrun = W;
+    for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
+        NlpDev di = d;
+        di.wl = Li[cur];
+        hipLaunchKernelGGL(ipm_rows_A, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
+        hipLaunchKernelGGL(ipm_world_A, dim3(nrun), dim3(64), 0, p->stream, di, ns);
+        hipLaunchKernelGGL(ipm_rows_B, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
+        hipLaunchKernelGGL(ipm_world_B, dim3(nrun), dim3(64), 0, p->stream, di);
+        // Round 0 of the line search for every running world, then one host synchronisation. The
+        // worlds still searching after it (the tail of the backtracking) run the remaining rounds
+        // without one: a few of them all remaining trials at once (speculative round, ipm_world_Cs),
+        // more of them round by round with grids sized by round 0's count and the list lengths in
+        // device memory (cnt[4 + r & 1]). Either way the arithmetic is that of sequential rounds.
+        int nnext = 0, nsearch = 0;
+        {
+            NlpDev dc = d;
+            dc.wl = Li[cur];
+            dc.wl_run = Li[1 - cur];
+            dc.wl_search = Ls[1];
+            dc.ls0 = 1;
+            dc.lcount_out = d.cnt + 5;
+            if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, dim3(p->T, nrun), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
+            else hipLaunchKernelGGL(eval_kernel_t<double>, dim3(p->T, nrun), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
+            hipLaunchKernelGGL(ipm_rows_C, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, dc);
+            hipLaunchKernelGGL(ipm_world_C, dim3(nrun), dim3(64), 0, p->stream, dc);
             HIPCK(hipStreamSynchronize(p->stream));
-            if (ls == 0 && it > 0 && ((volatile int*)p->h_flags)[1] == 0) {
-                done = true;  // every world converged, hit the cap or failed at the previous iteration
-                break;
-            }
-            if (((volatile int*)p->h_flags)[0] == 0) break;
+            nnext = ((volatile int*)p->h_flags)[0];
+            nsearch = ((volatile int*)p->h_flags)[1];
         }
-        if (done) break;
-        p->h_flags[1] = 0;  // the previous world_D completed before the synchronisation above
-        hipLaunchKernelGGL(ipm_rows_D, rows, dim3(ROW_THREADS), 0, p->stream, d);
-        hipLaunchKernelGGL(ipm_world_D, dim3(W), dim3(64), 0, p->stream, d);
+        if (nsearch > 0 && nsearch <= NSPEC && p->spec) {
+            NlpDev ds = d;
+            ds.wl = Ls[1];
+            const int ny = nsearch * d.K;
+            if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, dim3(p->T, ny), dim3(EVAL_THREADS), 0, p->stream, ds, 3);
+            else hipLaunchKernelGGL(eval_kernel_t<double>, dim3(p->T, ny), dim3(EVAL_THREADS), 0, p->stream, ds, 3);
+            hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, ny), dim3(ROW_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(ipm_world_Cs, dim3(nsearch), dim3(64), 0, p->stream, ds);
+            hipLaunchKernelGGL(ipm_copy_spec, dim3(64, nsearch), dim3(256), 0, p->stream, ds);
+        } else if (nsearch > 0) {
+            for (int ls = 1; ls < d.opt.max_ls; ls++) {
+                NlpDev dc = d;
+                dc.wl = Ls[ls & 1];
+                dc.lcount = d.cnt + 4 + (ls & 1);
+                dc.wl_search = Ls[(ls + 1) & 1];
+                dc.lcount_out = d.cnt + 4 + ((ls + 1) & 1);
+                dc.ls0 = 0;
+                if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
+                else hipLaunchKernelGGL(eval_kernel_t<double>, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
+                hipLaunchKernelGGL(ipm_rows_C, dim3(d.nblk, nsearch), dim3(ROW_THREADS), 0, p->stream, dc);
+                hipLaunchKernelGGL(ipm_world_C, dim3(nsearch), dim3(64), 0, p->stream, dc);
+            }
+        }
+        if (nnext == 0) break;  // every world converged, hit the cap or failed
+        hipLaunchKernelGGL(ipm_rows_D, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
+        hipLaunchKernelGGL(ipm_world_D, dim3(nrun), dim3(64), 0, p->stream, di);
         HIPCK(hipGetLastError());
+        cur = 1 - cur;
+        nrun = nnext;
     }
     // feasibility re-check and the sliced link centres at the final iterate (the current slot's,
     // armour_joint_position_center.out payload)
@@ -745,11 +830,25 @@ int armour_get_reach_dump(armour_planner* p, double* dump, int capacity) {
     return p->nops;
 }
 
+int armour_get_monomial_counts(armour_planner* p, int w, int* link_counts, int* torque_counts) {
+    DeviceScope device_scope(p);
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
+    if (w < 0 || w >= p->W) return fail(ARMOUR_E_ARG, "world index out of range");
+    const size_t j0 = (size_t)w * p->T;
+    if (link_counts)
+        HIPCK(hipMemcpy(link_counts, p->ro.link_cnt + j0 * p->NJ, sizeof(int) * p->T * p->NJ, hipMemcpyDeviceToHost));
+    if (torque_counts)
+        HIPCK(hipMemcpy(torque_counts, p->ro.tq_cnt + j0 * NF, sizeof(int) * p->T * NF, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int armour_get_reach_occupancy(armour_planner* p, long long* used, long long* caps, int n) {
     DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
-    if (!p->lane_engine || !p->d_occ) return fail(ARMOUR_E_STATE, "occupancy is recorded by the bundle engine only");
+    if (!p->lane_engine || !p->d_occ)
+        return fail(ARMOUR_E_STATE, "occupancy is recorded by the bundle engine only (this batch ran on the per-job engine)");
     unsigned long long o[8] = {0};
     HIPCK(hipMemcpy(o, p->d_occ, sizeof(o), hipMemcpyDeviceToHost));
     const long long u[ARMOUR_OCC_COUNT] = {(long long)o[0], (long long)o[1], (long long)o[2], (long long)o[3],

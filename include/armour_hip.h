@@ -135,6 +135,9 @@ int armour_get_link_centers(armour_planner* p, int w, double* centers);       /*
 int armour_get_link_generators(armour_planner* p, int w, double* gens);       /* [T][NJ][3][6] */
 int armour_get_torque_radius(armour_planner* p, int w, double* radius);       /* [T][7] */
 int armour_num_joints(const armour_planner* p);
+/* k-only monomials of world w's link PZs [T][NJ] and torque PZs [T][7] after reduce_link_PZ /
+ * reduce (the M_links, M_tau of SURVEY.md §8(d)'s per-plan byte count); either may be null */
+int armour_get_monomial_counts(armour_planner* p, int w, int* link_counts, int* torque_counts);
 /* the 28 trailing values of armour_constraints.out (armour_main.cu:385-396): per joint
  * [lb + qe, ub - qe] then per joint [-v + qde, v - qde] */
 int armour_get_joint_bounds(const armour_planner* p, double* bounds28);

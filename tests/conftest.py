@@ -47,3 +47,23 @@ def load_golden(name):
 
 def world_of(fx):
     return fx["q0"], fx["qd0"], fx["qdd0"], fx["q_des"], fx["obstacles"]
+
+
+class engine:
+    """context manager: planners created inside use reach engine `name` ("lane": the bundle
+    engine, "job": the per-job engine; planner.hip picks by batch size otherwise)"""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.prev = os.environ.get("ARMOUR_ENGINE")
+        if self.name:
+            os.environ["ARMOUR_ENGINE"] = self.name
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is None:
+            os.environ.pop("ARMOUR_ENGINE", None)
+        else:
+            os.environ["ARMOUR_ENGINE"] = self.prev

@@ -21,6 +21,15 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def set_robot(robot_struct=None):
+    """robot tables (armour_amd.robot_tables.to_struct) for the following reach_job calls; None:
+    the built-in Kinova Gen3"""
+    global NJ
+    if lib().emu_set_robot(ctypes.byref(robot_struct) if robot_struct is not None else None) != 0:
+        raise ValueError("invalid robot tables")
+    NJ = int(robot_struct.num_joints) if robot_struct is not None else 7
+
+
 def reach_job(world, T, t, fused=True):
     """Outputs of job (world, t) as the kernel writes them (fused: the program's cross products
     as single ops, else composed from views / products / differences / stack)."""

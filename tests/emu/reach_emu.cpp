@@ -15,16 +15,29 @@ extern "C" void emu_set_dump(double* d) { g_dump = d; }
 extern "C" void emu_set_unfused(int u) { g_unfused = u; }
 extern "C" void emu_set_stats(int* st) { armour::g_op_stats = st; }
 extern "C" void emu_set_hash_sink(void (*f)(int, const uint64_t*, int)) { armour::g_hash_sink = f; }
+static RobotParams g_rp;
+static bool g_init = false;
+static ProgramBuilder g_pbf, g_pbu;  // fused / composed cross products
+// robot tables (include/armour_hip.h armour_robot); null: the built-in Kinova Gen3
+extern "C" int emu_set_robot(const armour_robot* r) {
+    if (r) {
+        if (!robot_from_tables(*r, g_rp)) return -1;
+    } else {
+        kinova_gen3(g_rp);
+    }
+    g_init = true;
+    g_pbf = ProgramBuilder();
+    g_pbu = ProgramBuilder();
+    return 0;
+}
 extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, const double* qdd0,
                          double* link_gens, double* link_center, double* link_rad, int* link_cnt,
                          uint16_t* link_hash, double* link_coef, double* tq_center, double* tq_rad,
                          int* tq_cnt, uint16_t* tq_hash, double* tq_coef, double* torque_radius,
                          long* arena_used, double* arena_bytes, int* nops, int* nslots) {
-    static RobotParams rp;
-    static bool init = false;
-    if (!init) { kinova_gen3(rp); init = true; }
-    static ProgramBuilder pbf, pbu;  // fused / composed cross products
-    ProgramBuilder& pb = g_unfused ? pbu : pbf;
+    if (!g_init) emu_set_robot(nullptr);
+    RobotParams& rp = g_rp;
+    ProgramBuilder& pb = g_unfused ? g_pbu : g_pbf;
     if (pb.ops.empty()) {
         pb.fused = !g_unfused;
         pb.build(rp);

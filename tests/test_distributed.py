@@ -44,13 +44,13 @@ def _worker(rank, ws, port, n, q):
     mine = D.shard(n, rank, ws)
     # fake per-world plan results: world i has cost (i * 7919 % 13) and is feasible when i % 3 != 0
     res = [dict(k_opt=np.full(7, i / 100), cost=float(i * 7919 % 13), feasible=i % 3 != 0, status=0) for i in mine]
-    allrec, best = D.gather(D.records(res), dist)
+    allrec, best = D.gather(D.records(res), dist, total=n)
     q.put((rank, allrec, best))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [8, 6])
+@pytest.mark.parametrize("n", [8, 7, 256])
 def test_gather_world_size_2(n):
     ws = 2
     ctx = mp.get_context("spawn")

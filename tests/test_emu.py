@@ -66,3 +66,26 @@ def test_fused_cross_products_equal_composed():
         for k in ("link_gens", "link_center", "link_rad", "link_cnt", "link_hash", "link_coef", "tq_center", "tq_rad",
                   "tq_cnt", "tq_hash", "tq_coef", "torque_radius"):
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_emulated_program_fetch_matches_oracle():
+    """the same program built from the Fetch arm's URDF tables (8 links, the fixed gripper last):
+    link generators of every link and the torque radius against the oracle"""
+    from armour_amd import robot_tables as RT
+
+    fetch = RT.load_json(os.path.join(os.path.dirname(__file__), "golden", "robot_fetch.json"))
+    world = make_world(31, 8, robot=RT.geometry(fetch))
+    Tf = 40
+    P = OraclePlanner(*world, T=Tf, threads=4, robot=RT.to_struct(fetch))
+    P.reach()
+    NJ = P.NJ
+    lg_o = P.get(0).reshape(Tf, NJ, 18)
+    emu.set_robot(RT.to_struct(fetch))
+    try:
+        for t in (0, 17, 39):
+            o = emu.reach_job(world, Tf, t)
+            assert o["err"] == 0
+            np.testing.assert_allclose(o["link_gens"], lg_o[t], rtol=0, atol=1e-14)
+            np.testing.assert_allclose(o["torque_radius"], P.torque_radius()[t], rtol=0, atol=1e-12)
+    finally:
+        emu.set_robot(None)

@@ -16,6 +16,7 @@ import pytest
 
 import armour_amd as A
 import boundary_worlds as B
+from conftest import engine
 from oracle import OraclePlanner
 from test_boundary import load, world
 from test_gpu_drop_in import run, write_input
@@ -24,11 +25,12 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-9
 
 
-def compare_set(name, min_near):
+def compare_set(name, min_near, eng):
     fx = load(name)
     T, W, O = int(fx["T"]), len(fx["kinds"]), fx["obstacles"].shape[1]
     worlds = [world(fx, w) for w in range(W)]
-    P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    with engine(eng):
+        P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
     P.reach(worlds)
     near = 0
     refs = []
@@ -73,20 +75,26 @@ def compare_set(name, min_near):
     return near, infeasible
 
 
-def test_boundary_small():
-    compare_set("boundary_small_T20_O6", 50)
+ENGINES = ["lane", "job"]  # both reach engines (planner.hip picks by batch size)
 
 
-def test_boundary_config2():
+@pytest.mark.parametrize("eng", ENGINES)
+def test_boundary_small(eng):
+    compare_set("boundary_small_T20_O6", 50, eng)
+
+
+@pytest.mark.parametrize("eng", ENGINES)
+def test_boundary_config2(eng):
     """BASELINE configs[1] sizes (T=100, O=20) on the decision boundary"""
-    near, infeasible = compare_set("boundary_config2_T100_O20", 1000)
-    print(f"config 2 boundary: {near} near-threshold rows compared, {infeasible} infeasible plans")
+    near, infeasible = compare_set("boundary_config2_T100_O20", 1000, eng)
+    print(f"config 2 boundary ({eng}): {near} near-threshold rows compared, {infeasible} infeasible plans")
 
 
-def test_boundary_config3():
+@pytest.mark.parametrize("eng", ENGINES)
+def test_boundary_config3(eng):
     """BASELINE configs[2] sizes (T=200, O=40) on the decision boundary"""
-    near, infeasible = compare_set("boundary_config3_T200_O40", 1000)
-    print(f"config 3 boundary: {near} near-threshold rows compared, {infeasible} infeasible plans")
+    near, infeasible = compare_set("boundary_config3_T200_O40", 1000, eng)
+    print(f"config 3 boundary ({eng}): {near} near-threshold rows compared, {infeasible} infeasible plans")
 
 
 def test_drop_in_writes_minus_one_for_infeasible(tmp_path):

@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import armour_amd as A
+from conftest import engine
 
 pytestmark = pytest.mark.gpu
 DEBUG = (np.array([-1.0, -1, -1, -1, 1, 1, 1]), np.array([1.0, 1, 1, -1, -1, -1, -1]), np.full(7, 2.0))
@@ -27,7 +28,8 @@ def test_full_range_headroom():
     largest use of every buffer stays below 80 % of its capacity"""
     T, O = 100, 20
     B = A.default_batch(T)
-    P = A.Planner(T=T, max_obstacles=O, max_worlds=B)
+    with engine("lane"):  # the last batch (19 worlds) would take the per-job engine
+        P = A.Planner(T=T, max_obstacles=O, max_worlds=B)
     worst = {}
     for s0 in range(0, 1000, B):
         worlds = [A.make_world(s, O, profile="survey") for s in range(s0, min(1000, s0 + B))]
@@ -43,7 +45,8 @@ def test_full_range_headroom():
 
 def test_debug_state_headroom():
     """the reference's debug state (qd0 = +-1, qdd0 = 2) at the drop-in's T = 128"""
-    P = A.Planner(T=128, max_obstacles=10, max_worlds=1)
+    with engine("lane"):  # the bundle engine records occupancy (and has the union inflation)
+        P = A.Planner(T=128, max_obstacles=10, max_worlds=1)
     res, _ = P.plan([debug_world(10)])
     occ = P.occupancy()
     print(occ)
@@ -57,7 +60,8 @@ def _planner(T, O, W, ccap=None):
     else:
         os.environ["ARMOUR_LANE_CCAP"] = str(ccap)
     try:
-        return A.Planner(T=T, max_obstacles=O, max_worlds=W)
+        with engine("lane"):
+            return A.Planner(T=T, max_obstacles=O, max_worlds=W)
     finally:
         os.environ.pop("ARMOUR_LANE_CCAP", None)
 

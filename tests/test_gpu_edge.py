@@ -88,3 +88,29 @@ def test_concurrent_planners_match_sequential():
         for r0, r1 in zip(seq[b], out[b]):
             assert np.array_equal(r0["k_opt"], r1["k_opt"]) and r0["iterations"] == r1["iterations"]
             assert r0["feasible"] == r1["feasible"] and r0["status"] == r1["status"]
+
+
+def test_speculative_line_search_matches_sequential():
+    """The tail's speculative line-search round (all remaining trials of the few searching worlds
+    at once, planner.hip run_solver) gives bitwise the plans of sequential rounds
+    (ARMOUR_NO_SPEC), on full-range worlds whose line searches run long."""
+    import os
+
+    T, O = 40, 10
+    worlds = [A.make_world(s, O, profile="survey") for s in range(48)]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
+    res_s, _ = P.plan(worlds)
+    g_s = [P.constraints(w) for w in range(len(worlds))]
+    c_s = [P.link_centers(w) for w in range(len(worlds))]
+    os.environ["ARMOUR_NO_SPEC"] = "1"
+    try:
+        Q = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
+    finally:
+        del os.environ["ARMOUR_NO_SPEC"]
+    res_q, _ = Q.plan(worlds)
+    assert sum(r["evaluations"] - r["iterations"] > 1 for r in res_q) > 0, "no world backtracked"
+    for w, (a, b) in enumerate(zip(res_s, res_q)):
+        assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"]
+        assert (a["iterations"], a["evaluations"], a["status"], a["feasible"]) == \
+            (b["iterations"], b["evaluations"], b["status"], b["feasible"])
+        assert np.array_equal(g_s[w], Q.constraints(w)) and np.array_equal(c_s[w], Q.link_centers(w))

@@ -12,7 +12,7 @@ import os
 
 import armour_amd as A
 from armour_amd import robot_tables as RT
-from conftest import golden_names, load_golden, world_of
+from conftest import engine, golden_names, load_golden, world_of
 from oracle import OraclePlanner
 
 pytestmark = pytest.mark.gpu
@@ -26,11 +26,16 @@ def collision_rows(T, O, NJ):
     return slice(7 * T, 7 * T + NJ * T * O)
 
 
+ENGINES = ["lane", "job"]  # both reach engines (planner.hip picks by batch size)
+
+
+@pytest.mark.parametrize("eng", ENGINES)
 @pytest.mark.parametrize("name", golden_names())
-def test_fixture(name):
+def test_fixture(name, eng):
     fx = load_golden(name)
     T, O = int(fx["T"]), fx["obstacles"].shape[0]
-    P = A.Planner(T=T, max_obstacles=max(O, 1), max_worlds=1)
+    with engine(eng):
+        P = A.Planner(T=T, max_obstacles=max(O, 1), max_worlds=1)
     world = world_of(fx)
     P.reach([world])
     np.testing.assert_allclose(P.torque_radius(0), fx["torque_radius"], rtol=0, atol=TOL)
@@ -55,10 +60,11 @@ def test_fixture(name):
     assert tm["reach_kernel_ms"] > 0 and tm["reach_bytes"] > 0
 
 
-def _compare_batch(T, O, seeds, xs, robot=None):
+def _compare_batch(T, O, seeds, xs, robot=None, eng=None):
     geo = RT.geometry(robot) if robot is not None else A.KINOVA
     worlds = [A.make_world(s, O, robot=geo) for s in seeds]
-    P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds), robot=robot)
+    with engine(eng):
+        P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds), robot=robot)
     P.reach(worlds)
     refs = []
     for w, world in enumerate(worlds):
@@ -82,9 +88,11 @@ def _compare_batch(T, O, seeds, xs, robot=None):
         np.testing.assert_allclose(r["k_opt"], ro["k_opt"], rtol=0, atol=1e-8)
 
 
-def test_config2_batch():
+@pytest.mark.parametrize("eng", ENGINES)
+def test_config2_batch(eng):
     """BASELINE configs[1]: Kinova, T=100, O=20"""
-    _compare_batch(100, 20, [11, 12, 13, 14], [np.zeros(7), np.array([0.5, 0.6, 0.7, 0.0, -0.5, -0.6, -0.7])])
+    _compare_batch(100, 20, [11, 12, 13, 14], [np.zeros(7), np.array([0.5, 0.6, 0.7, 0.0, -0.5, -0.6, -0.7])],
+                   eng=eng)
 
 
 def test_config2_bench_batch_sweep():
@@ -97,7 +105,8 @@ def test_config2_bench_batch_sweep():
 def test_config5_fetch_batch():
     """BASELINE configs[4]: the Fetch arm from its URDF (tests/golden/robot_fetch.json: 7 actuated
     joints + the fixed gripper), here at fp64 and reduced sizes (T=40, O=8); the full-size run is
-    `bench.py --robot fetch`"""
+    `bench.py --robot fetch`. Fetch's reach program does not fit the per-job engine's LDS pool, so
+    every batch size runs on the bundle engine (planner.hip job_fits)"""
     fetch = RT.load_json(os.path.join(GOLD, "robot_fetch.json"))
     _compare_batch(40, 8, [31, 32, 33], [np.zeros(7), np.linspace(-0.6, 0.6, 7)], robot=fetch)
 
@@ -108,9 +117,10 @@ def test_config5_fetch_full_size():
     _compare_batch(100, 20, list(range(600, 616)), [np.full(7, 0.3)], robot=fetch)
 
 
-def test_config3_batch():
+@pytest.mark.parametrize("eng", ENGINES)
+def test_config3_batch(eng):
     """BASELINE configs[2]: T=200, O=40 (MAX_OBSTACLE_NUM)"""
-    _compare_batch(200, 40, [21, 22], [np.full(7, -0.4)])
+    _compare_batch(200, 40, [21, 22], [np.full(7, -0.4)], eng=eng)
 
 
 def test_rerun_bitwise_and_batch_position_stable():
