@@ -71,6 +71,8 @@ def lib():
         L.armour_create_robot.argtypes = [ctypes.POINTER(Config), ctypes.c_void_p]
         L.armour_robot_builtin.argtypes = [ctypes.c_int, ctypes.c_void_p]
         L.armour_device_compute_units.argtypes = [ctypes.c_int]
+        L.armour_copy_bandwidth.restype = ctypes.c_double
+        L.armour_copy_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int]
         L.armour_destroy.argtypes = [ctypes.c_void_p]
         L.armour_last_error.restype = ctypes.c_char_p
         L.armour_num_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -95,7 +97,7 @@ def lib():
 
 
 # every symbol include/armour_hip.h declares (checked by tests/test_abi.py)
-ABI_SYMBOLS = ["armour_create", "armour_create_robot", "armour_robot_builtin", "armour_device_compute_units", "armour_destroy", "armour_last_error", "armour_num_constraints",
+ABI_SYMBOLS = ["armour_copy_bandwidth", "armour_create", "armour_create_robot", "armour_robot_builtin", "armour_device_compute_units", "armour_destroy", "armour_last_error", "armour_num_constraints",
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
@@ -108,6 +110,15 @@ def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
     n = lib().armour_device_compute_units(device)
     _check(min(0, n))
     return max(1, (waves * n * 64) // T)
+
+
+def copy_bandwidth(device: int = 0, nbytes: int = 2 << 30, reps: int = 10) -> float:
+    """device-to-device copy bandwidth in GB/s (read + write bytes / time) of a 16 B-per-lane
+    streaming copy kernel (armour_copy_bandwidth): the achievable HBM figure for roofline fractions"""
+    v = lib().armour_copy_bandwidth(device, nbytes, reps)
+    if v < 0:
+        raise ArmourError(f"armour_copy_bandwidth: {lib().armour_last_error().decode()}")
+    return v
 
 
 def _check(rc):
@@ -140,9 +151,9 @@ class Planner:
         self.O = 0
 
     def close(self):
-        if getattr(self, "h", None):
-            lib().armour_destroy(self.h)
-            self.h = None
+        if getattr(self, "h", None) and _LIB is not None:  # (module teardown may have cleared _LIB)
+            _LIB.armour_destroy(self.h)
+        self.h = None
 
     def __del__(self):
         self.close()
@@ -270,4 +281,4 @@ class Planner:
         return r
 
 
-__all__ = ["Planner", "ArmourError", "ARMOUR_E_CAPACITY", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]
+__all__ = ["Planner", "ArmourError", "ARMOUR_E_CAPACITY", "copy_bandwidth", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]

@@ -600,6 +600,46 @@ int armour_device_compute_units(int device) {
     return n;
 }
 
+// streaming copy, 16 B per lane per access, grid-stride (the achievable-HBM reference kernel)
+__global__ __launch_bounds__(256) void copy_kernel(const double2* __restrict__ src, double2* __restrict__ dst, long n) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+double armour_copy_bandwidth(int device, size_t bytes, int reps) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    struct Restore {
+        int d;
+        ~Restore() { if (d >= 0) (void)hipSetDevice(d); }
+    } restore{prev};
+    if (reps <= 0 || bytes < 16) return fail(ARMOUR_E_ARG, "bytes >= 16 and reps > 0");
+    if (hipSetDevice(device) != hipSuccess) return fail(ARMOUR_E_HIP, "hipSetDevice failed (no device?)");
+    const long n = (long)(bytes / 16);
+    double2 *a = nullptr, *b = nullptr;
+    hipEvent_t e0, e1;
+    if (hipMalloc((void**)&a, n * 16) != hipSuccess) return fail(ARMOUR_E_HIP, "hipMalloc failed");
+    if (hipMalloc((void**)&b, n * 16) != hipSuccess) { (void)hipFree(a); return fail(ARMOUR_E_HIP, "hipMalloc failed"); }
+    (void)hipMemset(a, 0, n * 16);
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+    const dim3 grid(ncu * 8), blk(256);
+    hipLaunchKernelGGL(copy_kernel, grid, blk, 0, nullptr, a, b, n);
+    (void)hipEventRecord(e0, nullptr);
+    for (int r = 0; r < reps; r++) hipLaunchKernelGGL(copy_kernel, grid, blk, 0, nullptr, a, b, n);
+    (void)hipEventRecord(e1, nullptr);
+    const hipError_t err = hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    if (err != hipSuccess || ms <= 0) return fail(ARMOUR_E_HIP, "copy kernel failed");
+    return 2.0 * n * 16.0 * reps / (ms * 1e-3) / 1e9;
+}
+
 int armour_robot_builtin(int robot_id, armour_robot* out) {
     if (!out || robot_id != 0) return fail(ARMOUR_E_ARG, "unknown robot id / null output");
     RobotParams r;

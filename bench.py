@@ -3,12 +3,25 @@
 
 Metric (BASELINE.json): planning iterations/sec at 1/2/4/8 GPUs. One planning iteration = one
 complete plan of KPR/armour_main.cu (JRS -> PZ FK/RNEA -> torque radius -> hyperplanes -> NLP to
-termination -> feasibility re-check). A step = one batch of `--batch` synthetic random-obstacle
-worlds planned on each GPU (default: two whole waves of 64-job reach bundles) (weak scaling: every rank plans its own worlds); after each step the
-per-world records (k_opt, cost, feasible) are all-gathered over RCCL and rank 0 takes the argmin
-over feasible worlds (the only collective on this path).
+termination -> feasibility re-check). Worlds: SURVEY.md §8(d)'s synthetic generator as written
+(armour_amd.worlds, profile "survey": full start-state ranges, obstacles rejected only when they
+intersect the start configuration), so a share of the worlds is infeasible and the solver works
+against active constraints; the line reports the feasible fraction.
 
-Usage: python bench.py [--gpus N --steps K --warmup W --batch B]
+Modes
+  weak (default): every rank plans its own --batch worlds per planner per step (default: two
+      whole waves of 64-job reach bundles); `value` = all ranks' worlds / max-over-ranks step time.
+  strong (--total-worlds N, config 4): one fixed job of N worlds sharded over the ranks
+      (armour_amd.dist.shard), each rank's shard split over its planners.
+After each step the per-world records are all-gathered over RCCL and rank 0 takes the argmin over
+feasible worlds (the only collective on this path).
+
+Rank 0 at N = 1 also reports: the roofline of the reach kernel (timed alone after the timed region)
+and SURVEY §8(d)'s per-plan byte count B_plan = B_setup + E * B_eval; the measured copy peak;
+single-plan latency (the drop-in's use: one world per call) at T = 100 and 128 and the wall time of
+the armour_main process; the CPU baseline (the oracle on config 1, 1 thread and the box's share).
+
+Usage: python bench.py [--gpus N --steps K --warmup W --batch B --planners P --total-worlds N]
        (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 Prints ONE JSON line on rank 0.
 """
@@ -17,7 +30,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import threading
 import time
 
@@ -27,6 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "armour-dev_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+C_PAIRS = 36           # generator pairs of a buffered obstacle (KPR/CollisionChecking.cu:26-39)
 
 
 def parse():
@@ -35,38 +51,66 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
-                    help="worlds per GPU per step (0: two whole bundle waves of the device, floor(2 * CUs * 64 / T): "
+                    help="worlds per planner per step (0: two whole bundle waves of the device, floor(2 * CUs * 64 / T): "
                          "327 on MI355X at T=100)")
     ap.add_argument("--planners", type=int, default=2,
-                    help="planners per GPU planning their own --batch concurrently (one HIP stream each, "
-                         "one host thread each); 2 overlaps one planner's solver with the other's reach")
+                    help="planners per GPU planning their own batch concurrently (one HIP stream and one host thread "
+                         "each); 2 overlaps one planner's solver with the other's reach")
+    ap.add_argument("--total-worlds", type=int, default=0,
+                    help="strong scaling (config 4): one job of this many worlds sharded over the ranks")
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--O", type=int, default=20)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
+    ap.add_argument("--profile", default="survey", choices=["survey", "default"],
+                    help="world generator: survey = SURVEY §8(d) as written; default = half start-state ranges and "
+                         "5 cm start clearance (the round-1 workload, every world feasible)")
     ap.add_argument("--robot", default="kinova", choices=["kinova", "fetch"],
                     help="kinova: built-in Gen3 tables (configs 1-4); fetch: tests/golden/robot_fetch.json, the "
                          "Fetch arm from its URDF (config 5, at fp64)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU-baseline leg (0: skip)")
+    ap.add_argument("--no-extras", action="store_true", help="skip the N=1 extras (latency, copy peak, roofline)")
     return ap.parse_args()
 
 
-def cpu_baseline(worlds, T, seconds, robot=None):
-    """Oracle (CPU restatement of the reference path, oracle/) on the host cores: whole plans of
-    the same worlds until `seconds` of work, OpenMP threads = the box's CPU share (<= 16)."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(seconds, robot=None, geo=None):
+    """The oracle (CPU restatement of the reference path, oracle/) planning BASELINE config 1
+    (Kinova, T=100, O=10, one plan at a time) from the same generator: one leg on 1 thread, one on
+    the box's CPU share (<= 16 threads; the reference runs 32 OpenMP threads, Parameters.h:35)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import armour_amd as A
     from oracle import OraclePlanner  # test/baseline infrastructure only
 
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    done, t0 = 0, time.perf_counter()
-    for w in worlds:
-        P = OraclePlanner(*w, T=T, threads=threads, robot=robot)
-        P.reach()
-        P.plan()
-        done += 1
-        if time.perf_counter() - t0 > seconds and done >= 2:
-            break
-    dt = time.perf_counter() - t0
-    return dict(value=done / dt, unit="plans/s", cores=threads, kind="port",
-                sample=f"{done} full plans (oracle C++ restatement, T={T}, O={len(worlds[0][4])}) in {dt:.1f}s")
+    share = max(1, min(16, len(os.sched_getaffinity(0))))
+    legs = {}
+    seed = 10_000
+    for threads in (1, share):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            w = A.make_world(seed, 10, robot=geo, profile="survey")
+            seed += 1
+            P = OraclePlanner(*w, T=100, threads=threads, robot=robot)
+            P.reach()
+            P.plan()
+            done += 1
+            if time.perf_counter() - t0 > seconds and done >= 1:
+                break
+        dt = time.perf_counter() - t0
+        legs[threads] = (done / dt, done, dt)
+    v, done, dt = legs[share]
+    v1, done1, dt1 = legs[1]
+    return dict(value=v, unit="plans/s", cores=share, kind="port", cpu_model=cpu_model(),
+                sample=f"config 1 (Kinova, T=100, O=10): {done} full plans of the oracle C++ restatement in {dt:.1f}s on "
+                       f"{share} threads",
+                one_thread=dict(value=v1, unit="plans/s", sample=f"{done1} plans in {dt1:.1f}s"))
 
 
 def lib_digest():
@@ -77,20 +121,78 @@ def lib_digest():
     return hashlib.sha1(open(LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
-def traffic_record(T, O, batch):
-    """HBM traffic per reach_kernel launch from the newest committed PMC summary of the same
-    workload AND the same library build (profiles/r*_reach_traffic.json, made by tools/gpu_prof.sh
-    + tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected); None if
-    there is none."""
+def traffic_record(T, O, batch, profile):
+    """HBM traffic per reach-kernel launch from the newest committed PMC summary of the same
+    workload AND library build (profiles/r*_reach_traffic.json, tools/pmc_traffic.py: separate
+    FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected); None if there is none."""
     import glob
 
     best = None
     digest = lib_digest()
     for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_reach_traffic.json"))):
         rec = json.load(open(fn))
-        if rec.get("config") == dict(T=T, O=O, batch=batch) and rec.get("lib_sha1") == digest:
+        if (rec.get("config") == dict(T=T, O=O, batch=batch) and rec.get("lib_sha1") == digest
+                and rec.get("profile", "default") == profile):
             best = (fn, rec)
     return best
+
+
+def latency(A, O, robot, geo):
+    """the drop-in's use: one world per call (KSI/uarmtd_planner.m runs one armour_main per plan)"""
+    out = {}
+    for T in (100, 128):
+        P = A.Planner(T=T, max_obstacles=O, max_worlds=1, robot=robot)
+        ws = [[A.make_world(50_000 + s, O, robot=geo, profile="survey")] for s in range(8)]
+        P.plan(ws[0])
+        ms = []
+        for w in ws:
+            t0 = time.perf_counter()
+            P.plan(w)
+            ms.append((time.perf_counter() - t0) * 1e3)
+        out[f"T{T}_ms_per_plan"] = float(np.median(ms))
+        out[f"T{T}_ms_max"] = float(np.max(ms))
+        P.close()
+    exe = os.path.join(ROOT, "armour-dev_amd", "armour_amd", "armour_main")
+    if robot is None and os.path.exists(exe):
+        q0, qd0, qdd0, qdes, obs = A.make_world(50_000, O, geo, profile="survey")
+        with tempfile.TemporaryDirectory() as d:
+            with open(os.path.join(d, "armour.in"), "w") as f:
+                for v in (q0, qd0, qdd0, qdes):
+                    f.write(" ".join(f"{x:.10f}" for x in v) + "\n")
+                f.write(f"{len(obs)}\n")
+                for o in obs:
+                    f.write(" ".join(f"{x:.10f}" for x in o) + "\n")
+            walls = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r = subprocess.run([exe, d], capture_output=True, text=True, timeout=120)
+                walls.append((time.perf_counter() - t0) * 1e3)
+                if r.returncode != 0:
+                    walls = None
+                    break
+            if walls:
+                rep = open(os.path.join(d, "armour.out")).read().split()
+                out["armour_main_wall_ms"] = float(np.median(walls))
+                out["armour_main_reported_ms"] = float(rep[-1])
+                out["armour_main_T"] = 128
+    return out
+
+
+def per_plan_bytes(P, res, T, O, NJ, reach_bytes, nsample=8):
+    """B_plan = B_setup + E * B_eval with E the constraint + Jacobian evaluations of
+    the solver (recorded per world), M_links / M_tau the k-only monomials kept per world"""
+    m = 7 * T + NJ * T * O + 28
+    ml, mt = [], []
+    for w in range(min(nsample, len(res))):
+        lk, tq = P.monomial_counts(w)
+        ml.append(int(lk.sum()))
+        mt.append(int(tq.sum()))
+    M_links, M_tau = float(np.mean(ml)), float(np.mean(mt))
+    hyper = 40.0 * T * NJ * O * C_PAIRS
+    B_eval = hyper + (24 + 8) * M_links * 2 + (8 + 8) * M_tau * 2 + 8.0 * m * (1 + 7)
+    B_setup = hyper + 8.0 * T * NJ * 18 + reach_bytes
+    E = float(np.mean([r["evaluations"] for r in res]))
+    return dict(B_setup=B_setup, B_eval=B_eval, E=E, B_plan=B_setup + E * B_eval, M_links=M_links, M_tau=M_tau)
 
 
 def main():
@@ -113,49 +215,65 @@ def main():
     import armour_amd as A
     from armour_amd import dist as D
 
-    if a.batch <= 0:
-        a.batch = A.default_batch(a.T, local_rank)
-
-    # weak scaling: rank r plans worlds r*batch .. r*batch+batch-1 (armour_amd.dist.shard of the whole job)
     robot, geo, robot_name = None, A.KINOVA, "Kinova Gen3 7-DOF"
     if a.robot == "fetch":
         from armour_amd import robot_tables as RT
         robot = RT.load_json(os.path.join(ROOT, "tests", "golden", "robot_fetch.json"))
         geo = RT.geometry(robot)
         robot_name = "Fetch arm (URDF, 7 actuated + fixed gripper)"
-    # a.planners planners per GPU (one HIP stream each) plan their own batch concurrently from host
-    # threads (ctypes releases the GIL in armour_plan_batch); the GPU overlaps one planner's solver
-    # iterations with another's reach. The rank's worlds are split between them.
+
     P = a.planners
-    worlds_all = [A.make_world(i, a.O, robot=geo) for i in D.shard(a.batch * P * world_size, rank, world_size)]
-    subs = [worlds_all[p * a.batch:(p + 1) * a.batch] for p in range(P)]
-    worlds = subs[0]
-    planners = [A.Planner(T=a.T, max_obstacles=a.O, max_worlds=a.batch, device=local_rank, robot=robot)
-                for _ in range(P)]
-    planner = planners[0]
+    strong = a.total_worlds > 0
+    if strong:
+        mine = list(D.shard(a.total_worlds, rank, world_size))
+        per = -(-len(mine) // P)
+        subs_idx = [mine[p * per:(p + 1) * per] for p in range(P)]
+        subs_idx = [s for s in subs_idx if s]
+        P = len(subs_idx)
+        a.batch = max(len(s) for s in subs_idx)
+    else:
+        if a.batch <= 0:
+            a.batch = A.default_batch(a.T, local_rank)
+        mine = list(D.shard(a.batch * P * world_size, rank, world_size))
+        subs_idx = [mine[p * a.batch:(p + 1) * a.batch] for p in range(P)]
+    subs = [[A.make_world(i, a.O, robot=geo, profile=a.profile) for i in s] for s in subs_idx]
+    planners = [A.Planner(T=a.T, max_obstacles=a.O, max_worlds=len(s), device=local_rank, robot=robot) for s in subs]
+    n_rank = sum(len(s) for s in subs)
+    total_job = a.total_worlds if strong else a.batch * a.planners * world_size
+
+    def fail(exc):
+        print(f"bench: rank {rank}: {exc!r}", file=sys.stderr, flush=True)
+        if dist is not None:
+            os._exit(1)  # the other ranks' collectives cannot complete; end this rank at once
+        raise exc
 
     def plan_all():
-        # one step: every planner plans its batch; the collective below stays on this thread, so
-        # every rank issues it in the same order
+        # one step: every planner plans its batch from its own host thread (ctypes releases the GIL
+        # in armour_plan_batch); the collective below stays on this thread
         if P == 1:
-            res, tm = planner.plan(worlds)
+            res, tm = planners[0].plan(subs[0])
             return res, [tm]
-        out = [None] * P
+        out, errs = [None] * P, [None] * P
 
         def work(p):
-            out[p] = planners[p].plan(subs[p])
+            try:
+                out[p] = planners[p].plan(subs[p])
+            except BaseException as e:  # re-raised on the main thread
+                errs[p] = e
 
         ths = [threading.Thread(target=work, args=(p,)) for p in range(P)]
         for th in ths:
             th.start()
         for th in ths:
             th.join()
-        if any(o is None for o in out):
-            raise RuntimeError("a planner thread failed")
+        for e in errs:
+            if e is not None:
+                fail(e)
         return [r for o in out for r in o[0]], [o[1] for o in out]
 
     def gather(res):
-        return D.gather(D.records(res), dist, device="cuda" if dist is not None else None)
+        return D.gather(D.records(res), dist, device="cuda" if dist is not None else None,
+                        total=total_job if strong else None)
 
     def barrier():
         if dist is not None:
@@ -164,19 +282,22 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
-        # untimed: planners one after another, so first-launch costs do not pile up on one kernel
-        res = [r for p in range(P) for r in planners[p].plan(subs[p])[0]]
-        gather(res)
-    barrier()
-    t0 = time.perf_counter()
-    tms = []
-    for _ in range(a.steps):
-        res, tm = plan_all()
-        allrec, best = gather(res)
-        tms.extend(tm)
-    barrier()
-    elapsed = time.perf_counter() - t0
+    try:
+        for _ in range(a.warmup):
+            # untimed: planners one after another, so first-launch costs do not pile up on one kernel
+            res = [r for p in range(P) for r in planners[p].plan(subs[p])[0]]
+            gather(res)
+        barrier()
+        t0 = time.perf_counter()
+        tms = []
+        for _ in range(a.steps):
+            res, tm = plan_all()
+            allrec, best = gather(res)
+            tms.extend(tm)
+        barrier()
+        elapsed = time.perf_counter() - t0
+    except Exception as e:  # noqa: BLE001
+        fail(e)
     if dist is not None:
         import torch
 
@@ -186,52 +307,77 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
-    total_plans = a.steps * a.batch * P * world_size
-    # roofline of the dominant kernel (reach_kernel): algorithmic bytes = monomial bytes read and
-    # written by the PZ operators, timed with HIP events on the planner stream
-    rk_ms = float(np.mean([t["reach_kernel_ms"] for t in tms]))
-    rk_bytes = float(np.mean([t["reach_bytes"] for t in tms]))
-    achieved = rk_bytes / (rk_ms * 1e-3) / 1e9
+    total_plans = a.steps * total_job
+    value = total_plans / elapsed
     n_feas = int(allrec[:, 8].sum())
+    iters = [r["iterations"] for r in res]
     line = {
         "metric": "planning iterations/sec (7-DOF, 100 t-steps, 20 obs)",
-        "value": total_plans / elapsed,
+        "value": value,
         "unit": "plans/s",
         "n_gpus": world_size,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic random-obstacle worlds (armour_amd.worlds, seeds rank*batch+i)",
+        "data": f"synthetic random-obstacle worlds (armour_amd.worlds profile '{a.profile}', "
+                + ("seeds 0..total_worlds-1 sharded over ranks)" if strong else
+                   "seeds rank*batch*planners + i: every rank its own worlds)"),
         "config": {"workload": f"{robot_name}, T={a.T}, O={a.O} box obstacles, "
-                               + (f"{a.batch} worlds/GPU/step" if P == 1 else
-                                  f"{P} concurrent planners x {a.batch} worlds/GPU/step"),
-                   "num_time_steps": a.T, "obstacles": a.O, "worlds_per_gpu": a.batch * P,
-                   "planners_per_gpu": P, "worlds_per_planner": a.batch,
+                               + (f"one job of {a.total_worlds} worlds over {world_size} GPU(s)" if strong else
+                                  f"{P} concurrent planner(s) x {a.batch} worlds/GPU/step"),
+                   "num_time_steps": a.T, "obstacles": a.O, "worlds_per_gpu": n_rank,
+                   "planners_per_gpu": P, "worlds_per_planner": a.batch, "world_profile": a.profile,
                    "parallelism": f"world-sharded x{world_size}, RCCL all_gather of per-world records"},
         "breakdown_ms": {"reach": float(np.mean([t["reach_ms"] for t in tms])),
                          "nlp": float(np.mean([t["nlp_ms"] for t in tms])),
-                         "reach_kernel": rk_ms},
+                         "reach_kernel": float(np.mean([t["reach_kernel_ms"] for t in tms]))},
         "feasible_worlds": n_feas,
         "total_worlds_last_step": int(allrec.shape[0]),
-        "roofline": {"kernel": "reach_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "algorithmic_bytes_per_launch": rk_bytes, "launch_ms": rk_ms},
+        "feasible_fraction": n_feas / max(1, int(allrec.shape[0])),
+        "solver": {"mean_iterations": float(np.mean(iters)), "max_iterations": int(np.max(iters)),
+                   "mean_evaluations": float(np.mean([r["evaluations"] for r in res]))},
+        "roofline": None,
         "cpu_baseline": None,
     }
-    tr = traffic_record(a.T, a.O, a.batch) if a.robot == "kinova" else None
-    if tr is not None:
-        line["roofline"]["traffic"] = tr[1]["traffic_bytes_per_launch"]
-        line["roofline"]["traffic_source"] = os.path.relpath(tr[0], ROOT)
+    if world_size == 1 and not a.no_extras:
+        # roofline of the reach kernel timed alone (no other planner sharing the GPU): HIP events on
+        # the planner's stream around the launch (armour_timing.reach_kernel_ms)
+        solo, tm_solo = planners[0].plan(subs[0])
+        rk_ms, rk_bytes = tm_solo["reach_kernel_ms"], tm_solo["reach_bytes"]
+        achieved = rk_bytes / (rk_ms * 1e-3) / 1e9
+        pp = per_plan_bytes(planners[0], solo, a.T, a.O, planners[0].NJ, rk_bytes / len(subs[0]))
+        pp_ach = pp["B_plan"] * value / 1e9
+        line["roofline"] = {
+            "kernel": "lane_reach_kernel", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": rk_bytes,
+            "launch_ms": rk_ms, "worlds_per_launch": len(subs[0]), "timing": "HIP events, planner alone on the GPU",
+            "limiter": "memory latency: dependent load rounds per simplify step, not bandwidth (DESIGN.md §4)",
+            "per_plan": {**pp, "achieved_GBps": pp_ach, "frac": pp_ach / HBM_PEAK_GBS,
+                         "note": "SURVEY §8(d) B_plan x plans/s; counts the reference design's stored hyperplanes, "
+                                 "which this build forms in registers instead"},
+        }
+        tr = traffic_record(a.T, a.O, len(subs[0]), a.profile) if a.robot == "kinova" else None
+        if tr is not None:
+            line["roofline"]["traffic"] = tr[1]["traffic_bytes_per_launch"]
+            line["roofline"]["traffic_source"] = os.path.relpath(tr[0], ROOT)
+        try:
+            line["copy_peak_GBps"] = A.copy_bandwidth(local_rank)  # 2 x 2 GiB, 16 B/lane copy kernel
+        except Exception as e:  # noqa: BLE001
+            line["copy_peak_GBps"] = None
+            print(f"copy peak not measured: {e!r}", file=sys.stderr)
+        for p in planners[1:]:
+            p.close()
+        line["latency"] = latency(A, a.O, robot, geo)
     if a.cpu_seconds > 0 and world_size == 1:   # the CPU baseline is an N = 1 figure (rank 0 only)
         rs = None
         if robot is not None:
             from armour_amd import robot_tables as RT
             rs = RT.to_struct(robot)
-        line["cpu_baseline"] = cpu_baseline(worlds, a.T, a.cpu_seconds, robot=rs)
+        line["cpu_baseline"] = cpu_baseline(a.cpu_seconds, robot=rs, geo=geo)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

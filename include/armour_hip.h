@@ -14,6 +14,8 @@
 #ifndef ARMOUR_HIP_H
 #define ARMOUR_HIP_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -106,6 +108,11 @@ typedef struct armour_robot {
 /* compute units of a HIP device (< 0: error). The reach kernel runs one 64-job bundle per CU at a
  * time, so batches of whole bundle waves, W = k * CUs * 64 / num_time_steps worlds, fill the chip. */
 int armour_device_compute_units(int device);
+
+/* Diagnostics: device-to-device copy bandwidth of `bytes` (two buffers of that size) with a
+ * 16-B-per-lane streaming kernel, `reps` timed copies; GB/s of read + write bytes, or a negative
+ * ARMOUR_E_* code. The achievable HBM figure the roofline fractions are read against. */
+double armour_copy_bandwidth(int device, size_t bytes, int reps);
 
 /* built-in tables (robot id 0: Kinova Gen3 without gripper); 0 / ARMOUR_E_ARG */
 int armour_robot_builtin(int robot_id, armour_robot* out);

@@ -81,6 +81,8 @@ def test_create_without_device_fails_loudly():
         pass
     with pytest.raises(A.ArmourError):
         A.Planner(T=10, max_obstacles=2, max_worlds=1)
+    with pytest.raises(A.ArmourError):
+        A.copy_bandwidth(0, 1 << 20, 1)
 
 
 def test_bad_config_rejected_before_device():
