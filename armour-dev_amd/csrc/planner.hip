@@ -49,6 +49,8 @@ struct armour_planner {
     RobotParams rp;
     RobotParams* d_rp = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t rstream = nullptr;   // reach phase (the planner's stream unless CUs are reserved)
+    int reach_cus = 0;               // CUs the reach stream may use
     hipEvent_t ev[6];
     // reach program (ProgramBuilder::ops) on the device
     Op* d_prog = nullptr;
@@ -136,7 +138,32 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     p->NJ = p->rp.num_joints;
     p->Omax = cfg->max_obstacles;
     p->Wmax = cfg->max_worlds;
-    HIPCK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    {
+        // Concurrent planners share the GPU. The bundle reach kernel holds every CU it runs on for
+        // its whole launch (persistent, 2 workgroups x 78 KB LDS per CU), so another planner's solver
+        // kernels wait for it. ARMOUR_REACH_CU_RESERVE=k keeps k CUs out of the reach stream's CU mask
+        // for them; ARMOUR_SOLVER_PRIORITY=1 gives the solver stream the highest queue priority.
+        const char* pr = std::getenv("ARMOUR_SOLVER_PRIORITY");
+        int lo = 0, hi = 0;
+        HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        const int prio = (pr && std::atoi(pr) != 0) ? hi : 0;
+        HIPCK(hipStreamCreateWithPriority(&p->stream, hipStreamNonBlocking, prio));
+        const char* rv = std::getenv("ARMOUR_REACH_CU_RESERVE");
+        const int reserve = rv ? std::atoi(rv) : 0;
+        p->reach_cus = p->ncu;
+        if (reserve > 0 && reserve < p->ncu) {
+            std::vector<uint32_t> mask((p->ncu + 31) / 32, 0u);
+            for (int c = 0; c < p->ncu; c++) mask[c / 32] |= 1u << (c % 32);
+            for (int i = 0; i < reserve; i++) {
+                const int c = (int)((long)i * p->ncu / reserve);
+                mask[c / 32] &= ~(1u << (c % 32));
+            }
+            HIPCK(hipExtStreamCreateWithCUMask(&p->rstream, (uint32_t)mask.size(), mask.data()));
+            p->reach_cus = p->ncu - reserve;
+        } else {
+            p->rstream = p->stream;
+        }
+    }
     for (int i = 0; i < 6; i++) HIPCK(hipEventCreate(&p->ev[i]));
     const int T = p->T, NJ = p->NJ, Om = p->Omax > 0 ? p->Omax : 1, Wm = p->Wmax;
     int rc = 0;
@@ -250,7 +277,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         // per-job use (~16.5k monomials) times the union inflation, with margin
         lane::LaneArgs& la = p->la;
         const long bundles = ((long)Wm * T + lane::LG - 1) / lane::LG;
-        const long slots = (long)p->ncu * lane::LANE_WG_PER_CU;
+        const long slots = (long)p->reach_cus * lane::LANE_WG_PER_CU;
         p->lane_grid = (int)(bundles < slots ? bundles : slots);
         const char* hc = std::getenv("ARMOUR_LANE_HCAP");
         const char* cc = std::getenv("ARMOUR_LANE_CCAP");
@@ -387,21 +414,24 @@ static int upload_worlds(armour_planner* p, int W, const armour_world* worlds) {
 // reach set + bounds for the uploaded batch
 static int run_reach(armour_planner* p) {
     NlpDev& d = p->d;
+    // the reach phase on the reach stream (ordered after the uploads, which end in a host
+    // synchronisation of the planner stream; it ends in one itself)
+    hipStream_t rs = p->rstream;
     ReachArgs ra = p->ra;
     ra.W = p->W;
     ra.T = p->T;
     ra.q0 = p->q0;
     ra.qd0 = p->qd0;
     ra.qdd0 = p->qdd0;
-    HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, p->stream));
-    HIPCK(hipMemsetAsync(p->d_bytes, 0, sizeof(unsigned long long), p->stream));
-    if (p->d_occ) HIPCK(hipMemsetAsync(p->d_occ, 0, sizeof(unsigned long long) * 8, p->stream));
+    HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, rs));
+    HIPCK(hipMemsetAsync(p->d_bytes, 0, sizeof(unsigned long long), rs));
+    if (p->d_occ) HIPCK(hipMemsetAsync(p->d_occ, 0, sizeof(unsigned long long) * 8, rs));
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
     p->lane_engine = !(p->has_job && jobs <= p->job_max);
     const long nj = jobs * NF;
-    HIPCK(hipEventRecord(p->ev[3], p->stream));
-    hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, p->stream, p->d_rp, p->W, p->T, p->q0, p->qd0,
+    HIPCK(hipEventRecord(p->ev[3], rs));
+    hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
                        p->qdd0, p->d_jrs);
     ra.jrs = p->d_jrs;
     if (p->lane_engine) {
@@ -411,17 +441,17 @@ static int run_reach(armour_planner* p) {
         la.jrs = p->d_jrs;
         const long bundles = (jobs + lane::LG - 1) / lane::LG;
         const int lg = (int)(bundles < p->lane_grid ? bundles : p->lane_grid);
-        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3(lg), dim3(lane::LT), 0, p->stream, p->d_rp, la, p->ro);
+        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3(lg), dim3(lane::LT), 0, rs, p->d_rp, la, p->ro);
     } else {
-        hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, p->stream, p->d_rp, ra, p->ro);
+        hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, rs, p->d_rp, ra, p->ro);
     }
     HIPCK(hipGetLastError());
-    HIPCK(hipEventRecord(p->ev[4], p->stream));
+    HIPCK(hipEventRecord(p->ev[4], rs));
     std::vector<int> err(p->W);
     unsigned long long bytes = 0;
-    HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, p->stream));
-    HIPCK(hipMemcpyAsync(&bytes, p->d_bytes, sizeof(bytes), hipMemcpyDeviceToHost, p->stream));
-    HIPCK(hipStreamSynchronize(p->stream));
+    HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
+    HIPCK(hipMemcpyAsync(&bytes, p->d_bytes, sizeof(bytes), hipMemcpyDeviceToHost, rs));
+    HIPCK(hipStreamSynchronize(rs));
     {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, p->ev[3], p->ev[4]);
@@ -448,19 +478,19 @@ static int run_reach(armour_planner* p) {
         la.pool_rows *= RETRY_SCALE;
         la.wlist = p->d_wlist;
         la.nlist = (int)retry.size();
-        HIPCK(hipMemcpyAsync(p->d_wlist, retry.data(), sizeof(int) * retry.size(), hipMemcpyHostToDevice, p->stream));
-        HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, p->stream));
+        HIPCK(hipMemcpyAsync(p->d_wlist, retry.data(), sizeof(int) * retry.size(), hipMemcpyHostToDevice, rs));
+        HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, rs));
         const long bundles = ((long)retry.size() * p->T + lane::LG - 1) / lane::LG;
         const long g = std::max(p->lane_grid, RETRY_SCALE) / RETRY_SCALE;
-        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3((int)(bundles < g ? bundles : g)), dim3(lane::LT), 0, p->stream,
+        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3((int)(bundles < g ? bundles : g)), dim3(lane::LT), 0, rs,
                            p->d_rp, la, p->ro);
         HIPCK(hipGetLastError());
-        HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, p->stream));
-        HIPCK(hipStreamSynchronize(p->stream));
+        HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
+        HIPCK(hipStreamSynchronize(rs));
     }
     // constraint bounds from the (final) torque radii
     const long rows = (long)p->W * d.R;
-    hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, p->stream, d);
+    hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, rs, d);
     HIPCK(hipGetLastError());
     p->world_err.assign(p->W, 0);
     p->last_failed = 0;
@@ -679,6 +709,7 @@ void armour_destroy(armour_planner* p) {
     if (p->h_feas) (void)hipHostFree(p->h_feas);
     if (p->stream) {
         for (int i = 0; i < 6; i++) (void)hipEventDestroy(p->ev[i]);
+        if (p->rstream && p->rstream != p->stream) (void)hipStreamDestroy(p->rstream);
         (void)hipStreamDestroy(p->stream);
     }
     delete p;
