@@ -45,6 +45,12 @@ _WORLD_DTYPE = np.dtype({"names": ["q0", "qd0", "qdd0", "q_des", "num_obstacles"
                          "itemsize": ctypes.sizeof(World)})
 
 
+class ArmtdWorld(ctypes.Structure):
+    _fields_ = [("q0", ctypes.c_double * NF), ("qd0", ctypes.c_double * NF), ("q_des", ctypes.c_double * NF),
+                ("jrs_tables", _dp), ("k_range", ctypes.c_double * NF), ("num_obstacles", ctypes.c_int),
+                ("obstacles", _dp)]
+
+
 class Result(ctypes.Structure):
     _fields_ = [("k_opt", ctypes.c_double * NF), ("feasible", ctypes.c_int), ("solver_status", ctypes.c_int),
                 ("iterations", ctypes.c_int), ("evaluations", ctypes.c_int), ("cost", ctypes.c_double),
@@ -77,6 +83,12 @@ def lib():
         L.armour_last_error.restype = ctypes.c_char_p
         L.armour_num_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.armour_num_joints.argtypes = [ctypes.c_void_p]
+        L.armour_create_armtd.restype = ctypes.c_void_p
+        L.armour_create_armtd.argtypes = [ctypes.POINTER(Config)]
+        L.armour_plan_armtd_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ArmtdWorld),
+                                              ctypes.POINTER(Result), ctypes.POINTER(Timing)]
+        L.armour_reach_armtd_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ArmtdWorld),
+                                               ctypes.POINTER(Timing)]
         L.armour_plan_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Result),
                                         ctypes.POINTER(Timing)]
         L.armour_reach_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Timing)]
@@ -101,7 +113,8 @@ ABI_SYMBOLS = ["armour_copy_bandwidth", "armour_create", "armour_create_robot", 
                "armour_plan_batch", "armour_reach_batch", "armour_eval_constraints", "armour_get_constraints",
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
-               "armour_get_reach_dump", "armour_get_reach_occupancy", "armour_get_monomial_counts"]
+               "armour_get_reach_dump", "armour_get_reach_occupancy", "armour_get_monomial_counts",
+               "armour_create_armtd", "armour_plan_armtd_batch", "armour_reach_armtd_batch"]
 
 
 def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
@@ -133,10 +146,12 @@ def _ptr(a):
 class Planner:
     """Batched MI355X planner. A world is (q0, qd0, qdd0, q_des, obstacles[O, 12])."""
 
-    def __init__(self, T=100, max_obstacles=20, max_worlds=1, device=0, max_iter=0, robot=None):
+    def __init__(self, T=100, max_obstacles=20, max_worlds=1, device=0, max_iter=0, robot=None, _armtd=False):
         """robot: None (built-in Kinova Gen3 tables) or a robot-table dict (armour_amd.robot_tables)"""
         cfg = Config(0, T, max_obstacles, max_worlds, device, max_iter)
-        if robot is None:
+        if _armtd:
+            self.h = lib().armour_create_armtd(ctypes.byref(cfg))
+        elif robot is None:
             self.h = lib().armour_create(ctypes.byref(cfg))
         else:
             from .robot_tables import to_struct
@@ -183,19 +198,29 @@ class Planner:
         arr = self._worlds(worlds)
         res = (Result * len(worlds))()
         tm = Timing()
-        _check(lib().armour_plan_batch(self.h, len(worlds), arr, res, ctypes.byref(tm)))
+        _check(self._plan_call(self.h, len(worlds), arr, res, ctypes.byref(tm)))
+        return self._results(res), tm.as_dict()
+
+    def _plan_call(self, *a):
+        return lib().armour_plan_batch(*a)
+
+    @staticmethod
+    def _results(res):
         out = []
         for r in res:
             out.append(dict(k_opt=np.array(r.k_opt[:]), feasible=bool(r.feasible), status=r.solver_status,
                             iterations=r.iterations, evaluations=r.evaluations, cost=r.cost, kkt=r.kkt_error,
                             error=r.error))
-        return out, tm.as_dict()
+        return out
 
     def reach(self, worlds):
         arr = self._worlds(worlds)
         tm = Timing()
-        _check(lib().armour_reach_batch(self.h, len(worlds), arr, ctypes.byref(tm)))
+        _check(self._reach_call(self.h, len(worlds), arr, ctypes.byref(tm)))
         return tm.as_dict()
+
+    def _reach_call(self, *a):
+        return lib().armour_reach_batch(*a)
 
     def eval_constraints(self, w, x, jac=True):
         m = self.num_constraints(self.O)
@@ -281,4 +306,40 @@ class Planner:
         return r
 
 
-__all__ = ["Planner", "ArmourError", "ARMOUR_E_CAPACITY", "copy_bandwidth", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]
+class ArmtdPlanner(Planner):
+    """The ARMTD comparison planner (armour_create_armtd). A world is the content of one armtd.in:
+    (q0, qd0, q_des, jrs_tables[7, 6, T], k_range[7], obstacles[O, 12]) with the tables per joint
+    c_cos, g_cos, r_cos, c_sin, g_sin, r_sin (ACMP/armtd_main.cu:37-102)."""
+
+    def __init__(self, T=100, max_obstacles=20, max_worlds=1, device=0, max_iter=0):
+        super().__init__(T=T, max_obstacles=max_obstacles, max_worlds=max_worlds, device=device, max_iter=max_iter,
+                         _armtd=True)
+
+    def _worlds(self, worlds):
+        n = len(worlds)
+        arr = (ArmtdWorld * n)()
+        keep = []
+        for k, (q0, qd0, q_des, tab, kr, obs) in enumerate(worlds):
+            a = arr[k]
+            a.q0[:] = [float(v) for v in q0]
+            a.qd0[:] = [float(v) for v in qd0]
+            a.q_des[:] = [float(v) for v in q_des]
+            a.k_range[:] = [float(v) for v in kr]
+            t = np.ascontiguousarray(np.asarray(tab, dtype=np.float64).reshape(NF, 6, self.T))
+            o = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, 12))
+            keep += [t, o]
+            a.jrs_tables = _ptr(t)
+            a.num_obstacles = o.shape[0]
+            a.obstacles = _ptr(o) if o.shape[0] else None
+        self._keep = keep
+        self.O = arr[0].num_obstacles if n else 0
+        return arr
+
+    def _plan_call(self, *a):
+        return lib().armour_plan_armtd_batch(*a)
+
+    def _reach_call(self, *a):
+        return lib().armour_reach_armtd_batch(*a)
+
+
+__all__ = ["ArmtdPlanner", "Planner", "ArmourError", "ARMOUR_E_CAPACITY", "copy_bandwidth", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]

@@ -44,6 +44,10 @@ struct WorldState {
 
 struct NlpDev {
     int W, T, NJ, O, m, R, nblk, chunk;
+    // the ARMTD comparison planner (ACMP/NLPclass.cu): no torque rows (nt = 0, else NF * T),
+    // constant-acceleration extrema and cost with a per-world k_range [W][NF]
+    int armtd, nt;
+    const double* krange;
     int diag;               // diagnostics (ARMOUR_EVAL_SKIP): bit 0 skip slicing, bit 1 skip collision rows
     const RobotParams* rp;
     IpmOpts opt;

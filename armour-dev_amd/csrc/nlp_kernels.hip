@@ -162,7 +162,7 @@ __global__ void bounds_kernel(NlpDev d) {
     for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
         const int w = (int)(idx / d.R), r = (int)(idx % d.R);
         double L, U;
-        const int nt = NF * d.T, nc = d.T * d.NJ * d.O;
+        const int nt = d.nt, nc = d.T * d.NJ * d.O;
         if (r < nt) {
             const int t = r / NF, j = r % NF;
             const double tr = d.ro.torque_radius[((long)w * d.T + t) * NF + j];
@@ -219,6 +219,88 @@ __device__ double wrap_to_pi(double a) {
     while (w < -M_PI) w += 2 * M_PI;
     while (w > M_PI) w -= 2 * M_PI;
     return w;
+}
+
+// ARMTD comparison planner: constant-acceleration extrema (ACMP/Trajectory.cu:83-383, the
+// gradient with respect to k_actual = k_range * x as the reference) and cost (ACMP/NLPclass.cu:
+// 186-246), one thread; restated as in oracle/src/armtd.cpp
+__device__ __noinline__ void armtd_extrema_cost(const NlpDev& d, int w, const double* x, double* Gb, double* Jb,
+                                                double* fb, double* gradb) {
+    const RobotParams& rp = *d.rp;
+    const long off = (long)d.T * d.NJ * d.O;
+    const double* q0 = d.q0 + w * NF;
+    const double* qd0 = d.qd0 + w * NF;
+    const double* kr = d.krange + w * NF;
+    const double t_move = 0.5, t_total = 1.0, t_to_stop = t_total - t_move;
+    for (int i = 0; i < NF; i++) {
+        const double k_actual = kr[i] * x[i];
+        const double q_peak = q0[i] + qd0[i] * t_move + k_actual * t_move * t_move * 0.5;
+        const double q_dot_peak = qd0[i] + k_actual * t_move;
+        const double q_ddot_to_stop = -q_dot_peak / t_to_stop;
+        const double q_stop = q_peak + q_dot_peak * t_to_stop + 0.5 * q_ddot_to_stop * t_to_stop * t_to_stop;
+        const double t_mm = -qd0[i] / k_actual;
+        double q_max_tp, q_min_tp, qd_max_tp, qd_min_tp, g_q_max_tp, g_q_min_tp, g_qd_max_tp, g_qd_min_tp;
+        double q_max_ts, q_min_ts, qd_max_ts, qd_min_ts, g_q_max_ts, g_q_min_ts, g_qd_max_ts, g_qd_min_ts;
+        double qe0, qe1, gqe0, gqe1;
+        if (q_peak >= q0[i]) { qe0 = q0[i]; qe1 = q_peak; gqe0 = 0; gqe1 = 0.5 * t_move * t_move; }
+        else { qe0 = q_peak; qe1 = q0[i]; gqe0 = 0.5 * t_move * t_move; gqe1 = 0; }
+        if (t_mm > 0 && t_mm < t_move) {
+            if (k_actual >= 0) {
+                q_min_tp = q0[i] + qd0[i] * t_mm + 0.5 * k_actual * t_mm * t_mm;
+                q_max_tp = qe1;
+                g_q_min_tp = (0.5 * qd0[i] * qd0[i]) / (k_actual * k_actual);
+                g_q_max_tp = gqe1;
+            } else {
+                q_min_tp = qe0;
+                q_max_tp = q0[i] + qd0[i] * t_mm + 0.5 * k_actual * t_mm * t_mm;
+                g_q_min_tp = gqe0;
+                g_q_max_tp = (0.5 * qd0[i] * qd0[i]) / (k_actual * k_actual);
+            }
+        } else {
+            q_min_tp = qe0; q_max_tp = qe1; g_q_min_tp = gqe0; g_q_max_tp = gqe1;
+        }
+        if (q_dot_peak >= qd0[i]) { qd_min_tp = qd0[i]; qd_max_tp = q_dot_peak; g_qd_min_tp = 0; g_qd_max_tp = t_move; }
+        else { qd_min_tp = q_dot_peak; qd_max_tp = qd0[i]; g_qd_min_tp = t_move; g_qd_max_tp = 0; }
+        if (q_stop >= q_peak) {
+            q_min_ts = q_peak; q_max_ts = q_stop;
+            g_q_min_ts = 0.5 * t_move * t_move; g_q_max_ts = 0.5 * t_move * t_move + 0.5 * t_move * t_to_stop;
+        } else {
+            q_min_ts = q_stop; q_max_ts = q_peak;
+            g_q_min_ts = 0.5 * t_move * t_move + 0.5 * t_move * t_to_stop; g_q_max_ts = 0.5 * t_move * t_move;
+        }
+        if (q_dot_peak >= 0) { qd_min_ts = 0; qd_max_ts = q_dot_peak; g_qd_min_ts = 0; g_qd_max_ts = t_move; }
+        else { qd_min_ts = q_dot_peak; qd_max_ts = 0; g_qd_min_ts = t_move; g_qd_max_ts = 0; }
+        const bool a = q_min_tp <= q_min_ts, b = q_max_tp >= q_max_ts;
+        const bool c = qd_min_tp <= qd_min_ts, e = qd_max_tp >= qd_max_ts;
+        const double val[4] = {a ? q_min_tp : q_min_ts, b ? q_max_tp : q_max_ts, c ? qd_min_tp : qd_min_ts,
+                               e ? qd_max_tp : qd_max_ts};
+        const double grd[4] = {a ? g_q_min_tp : g_q_min_ts, b ? g_q_max_tp : g_q_max_ts, c ? g_qd_min_tp : g_qd_min_ts,
+                               e ? g_qd_max_tp : g_qd_max_ts};
+        for (int q = 0; q < 4; q++) {
+            const long row = off + q * NF + i;
+            Gb[row] = val[q];
+            for (int k = 0; k < NF; k++) Jb[row * NF + k] = k == i ? grd[q] : 0.0;
+        }
+    }
+    // cost: q_plan = q0 + qd0 * 0.5 + k_range * x * 0.125, wrapped joints summed first
+    double qp[NF];
+    for (int i = 0; i < NF; i++) qp[i] = q0[i] + qd0[i] * 0.5 + kr[i] * x[i] * 0.125;
+    double fv = 0.0;
+    bool first = true;
+    for (int pass = 1; pass >= 0; pass--)
+        for (int i = 0; i < NF; i++) {
+            if (rp.wrap_mask[i] != pass) continue;
+            const double dd = pass ? wrap_to_pi(d.qdes[w * NF + i] - qp[i]) : (d.qdes[w * NF + i] - qp[i]);
+            const double term = dd * dd;
+            fv = first ? term : fv + term;
+            first = false;
+        }
+    *fb = fv * rp.cost_scale;
+    for (int i = 0; i < NF; i++) {
+        const double dk = kr[i] * 0.125;
+        const double gv = rp.wrap_mask[i] ? (2 * wrap_to_pi(qp[i] - d.qdes[w * NF + i]) * dk) : (2 * (qp[i] - d.qdes[w * NF + i]) * dk);
+        gradb[i] = gv * rp.cost_scale;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -279,7 +361,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         ptab[tid][4] = (R)0.0; ptab[tid][5] = (R)1.0 * (R)1.0; ptab[tid][6] = (R)2.0 * xj; ptab[tid][7] = (R)3.0 * (xj * xj);
     }
     if (tid < NJ) lcnt[tid] = d.ro.link_cnt[jt * NJ + tid];
-    if (tid >= 32 && tid < 32 + NF) tcnt[tid - 32] = d.ro.tq_cnt[jt * NF + tid - 32];
+    if (tid >= 32 && tid < 32 + NF) tcnt[tid - 32] = d.nt ? d.ro.tq_cnt[jt * NF + tid - 32] : 0;  // ARMTD: no torque PZs
     for (int i = tid; i < NJ * 18; i += blockDim.x) lgen[i / 18][i % 18] = d.ro.link_gens[jt * NJ * 18 + i];
     for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
     __syncthreads();
@@ -345,7 +427,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         }
       } else {
         // torque rows (NLPclass.cu:304-309, 376-380)
-        if (u >= NF * 8) continue;
+        if (u >= NF * 8 || d.nt == 0) continue;
         const int j = u / 8, k = u % 8;
         const long base = jt * NF + j;
         R c = k == 0 ? d.ro.tq_center[base] : 0.0;
@@ -360,7 +442,9 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         }
       }
     }
-    if (tid == blockDim.x - 1 && t == 0) {
+    if (tid == blockDim.x - 1 && t == 0 && d.armtd) {
+        armtd_extrema_cost(d, w, x, Gb, Jb, fb, gradb);
+    } else if (tid == blockDim.x - 1 && t == 0) {
         // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267)
         const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
         const double* q0 = d.q0 + w * NF;
@@ -415,7 +499,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     // parts of d and delta they determine alone (delta's summands kept separate where the
     // reference's left-to-right sum needs them in order), then the per-(link, obstacle) scan only
     // completes them.
-    const long nt = (long)NF * d.T;
+    const long nt = d.nt;
     const bool coll = !(d.diag & 2);
     for (int u = tid; u < (coll ? NJ * LL_PLANES + O * OO_PLANES : 0); u += blockDim.x) {
         if (u < NJ * LL_PLANES) {
@@ -1173,13 +1257,15 @@ __global__ void feasible_kernel(NlpDev d, int* feasible) {
     __shared__ int bad;
     if (threadIdx.x == 0) bad = 0;
     __syncthreads();
-    const int nt = NF * d.T, nc = d.T * d.NJ * d.O;
+    const int nt = d.nt, nc = d.T * d.NJ * d.O;
+    // ARMTD's re-check covers the collision rows of links 0 .. NF-2 only (ACMP/NLPclass.cu:375)
+    const int nc_checked = d.armtd ? d.T * (NF - 1) * d.O : nc;
     for (int r = threadIdx.x; r < d.m; r += blockDim.x) {
         const double v = d.g[gidx(d, S.cur, w, r)];
         const long i = (long)w * d.R + r;
         bool b;
         if (r < nt) b = v < d.L[i] - rp.torque_violation || v > d.U[i] + rp.torque_violation;
-        else if (r < nt + nc) b = v > rp.collision_violation;
+        else if (r < nt + nc) b = r < nt + nc_checked && v > rp.collision_violation;
         else b = v < d.L[i] || v > d.U[i];
         if (b) atomicOr(&bad, 1);
     }

@@ -73,6 +73,8 @@ struct armour_planner {
     // bundle engine (lane_kernel.hip): default; ARMOUR_ENGINE=job selects the per-job reach_kernel
     bool lane_engine = true;  // the last batch ran on the bundle engine
     bool has_lane = false, has_job = false;  // engines with buffers
+    bool armtd = false;       // the ARMTD comparison planner (armour_create_armtd)
+    double* d_tables = nullptr;  // ARMTD: offline JRS tables [W][NF][6][T]
     long job_max = 0;         // batches of at most this many jobs (W x T) run on the per-job engine
     bool job_fits = true;     // the reach program's payload pool fits the per-job engine's LDS
     bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
@@ -117,8 +119,9 @@ constexpr int RETRY_SCALE = 4;
 // largest batch (jobs = worlds x T) that runs on the per-job engine; measured crossover, DESIGN.md §4
 constexpr long JOB_ENGINE_JOBS = 3072;
 
-static int planner_init(armour_planner* p, const armour_config* cfg, const armour_robot* robot) {
+static int planner_init(armour_planner* p, const armour_config* cfg, const armour_robot* robot, bool armtd = false) {
     p->cfg = *cfg;
+    p->armtd = armtd;
     if (!robot && cfg->robot != 0) return fail(ARMOUR_E_ARG, "unknown robot id");
     if (cfg->num_time_steps <= 0 || (cfg->num_time_steps % 2) != 0)
         return fail(ARMOUR_E_ARG, "num_time_steps must be a positive even number (KPR/Parameters.h:16)");
@@ -189,7 +192,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // reach program
     {
         ProgramBuilder pb;
-        pb.build(p->rp);
+        pb.build(p->rp, p->armtd);
         int pool = 0;
         const std::vector<int> off = pb.slot_offsets(&pool);
         {
@@ -288,7 +291,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         int pool = 0;
         {
             ProgramBuilder pb;
-            pb.build(p->rp);
+            pb.build(p->rp, p->armtd);
             (void)pb.slot_offsets(&pool);
         }
         la.pool_rows = pool + 9;
@@ -328,8 +331,17 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     d.NJ = NJ;
     d.ro = ro;
     if (cfg->max_iter > 0) d.opt.max_iter = cfg->max_iter;
+    d.armtd = p->armtd ? 1 : 0;
+    d.nt = p->armtd ? 0 : NF * T;
+    d.krange = nullptr;
+    if (p->armtd) {
+        d.opt.tol = 1e-7;  // IPOPT_OPTIMIZATION_TOLERANCE (ACMP/Parameters.h:42)
+        double* kr = nullptr;
+        if ((rc = p->alloc(&p->d_tables, (size_t)Wm * NF * 6 * T)) || (rc = p->alloc(&kr, (size_t)Wm * NF))) return rc;
+        d.krange = kr;
+    }
     d.lcs = (long)(jobs * NJ * 3);
-    const size_t mmax = (size_t)NF * T + (size_t)T * NJ * Om + NF * 4;
+    const size_t mmax = (size_t)d.nt + (size_t)T * NJ * Om + NF * 4;
     const size_t Rmax = mmax + NF;
     if ((rc = p->alloc(&d.L, Wm * Rmax)) || (rc = p->alloc(&d.U, Wm * Rmax)) || (rc = p->alloc(&d.g, 2 * Wm * mmax)) ||
         (rc = p->alloc(&d.J, 2 * Wm * mmax * NF)) || (rc = p->alloc(&d.f, 2 * (size_t)Wm)) ||
@@ -404,11 +416,37 @@ static int upload_worlds(armour_planner* p, int W, const armour_world* worlds) {
     NlpDev& d = p->d;
     d.W = W;
     d.O = O;
-    d.m = NF * p->T + p->T * p->NJ * O + NF * 4;
+    d.m = d.nt + p->T * p->NJ * O + NF * 4;
     d.R = d.m + NF;
     d.chunk = row_chunk();
     d.nblk = (d.R + d.chunk - 1) / d.chunk;
     return 0;
+}
+
+// the ARMTD batch: armour_world fields (qdd0 = 0) plus the JRS tables and k_range
+static int upload_armtd(armour_planner* p, int W, const armour_armtd_world* worlds) {
+    if (!p->armtd) return fail(ARMOUR_E_ARG, "not an ARMTD planner (armour_create_armtd)");
+    if (W <= 0 || W > p->Wmax || !worlds) return fail(ARMOUR_E_ARG, "num_worlds out of range");
+    std::vector<armour_world> base(W);
+    const size_t ntab = (size_t)NF * 6 * p->T;
+    std::vector<double> tab((size_t)W * ntab), kr((size_t)W * NF);
+    for (int w = 0; w < W; w++) {
+        if (!worlds[w].jrs_tables) return fail(ARMOUR_E_ARG, "null jrs_tables");
+        armour_world& b = base[w];
+        for (int i = 0; i < NF; i++) {
+            b.q0[i] = worlds[w].q0[i];
+            b.qd0[i] = worlds[w].qd0[i];
+            b.qdd0[i] = 0.0;
+            b.q_des[i] = worlds[w].q_des[i];
+            kr[(size_t)w * NF + i] = worlds[w].k_range[i];
+        }
+        b.num_obstacles = worlds[w].num_obstacles;
+        b.obstacles = worlds[w].obstacles;
+        std::memcpy(&tab[(size_t)w * ntab], worlds[w].jrs_tables, sizeof(double) * ntab);
+    }
+    HIPCK(hipMemcpyAsync(p->d_tables, tab.data(), sizeof(double) * tab.size(), hipMemcpyHostToDevice, p->stream));
+    HIPCK(hipMemcpyAsync((double*)p->d.krange, kr.data(), sizeof(double) * kr.size(), hipMemcpyHostToDevice, p->stream));
+    return upload_worlds(p, W, base.data());  // ends in a synchronisation: tab / kr outlive the copies
 }
 
 // reach set + bounds for the uploaded batch
@@ -431,8 +469,12 @@ static int run_reach(armour_planner* p) {
     p->lane_engine = !(p->has_job && jobs <= p->job_max);
     const long nj = jobs * NF;
     HIPCK(hipEventRecord(p->ev[3], rs));
-    hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
-                       p->qdd0, p->d_jrs);
+    if (p->armtd)
+        hipLaunchKernelGGL(jrs_armtd_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, rs, p->W, p->T, p->q0, p->d_tables,
+                           p->d_jrs);
+    else
+        hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
+                           p->qdd0, p->d_jrs);
     ra.jrs = p->d_jrs;
     if (p->lane_engine) {
         lane::LaneArgs la = p->la;
@@ -511,7 +553,7 @@ static int run_reach(armour_planner* p) {
 
 static int nside_count(const armour_planner* p) {
     // finite constraint sides: torque 2/row, collision 1/row, extrema 2/row, box 2/variable
-    return 2 * NF * p->T + p->T * p->NJ * p->O + 2 * 4 * NF + 2 * NF;
+    return 2 * p->d.nt + p->T * p->NJ * p->O + 2 * 4 * NF + 2 * NF;
 }
 
 // g and J of every world of the batch (eval_kernel_t): fp64, or float for the tolerance study
@@ -698,6 +740,23 @@ armour_planner* armour_create_robot(const armour_config* cfg, const armour_robot
     return p;
 }
 
+armour_planner* armour_create_armtd(const armour_config* cfg) {
+    if (!cfg) { fail(ARMOUR_E_ARG, "null config"); return nullptr; }
+    struct Restore {
+        int dev = -1;
+        Restore() { if (hipGetDevice(&dev) != hipSuccess) dev = -1; }
+        ~Restore() { if (dev >= 0) (void)hipSetDevice(dev); }
+    } restore;
+    armour_planner* p = new armour_planner();
+    if (planner_init(p, cfg, nullptr, true) != 0) {
+        std::string keep = g_err;
+        armour_destroy(p);
+        g_err = keep;
+        return nullptr;
+    }
+    return p;
+}
+
 void armour_destroy(armour_planner* p) {
     DeviceScope device_scope(p);
     if (!p) return;
@@ -715,7 +774,7 @@ void armour_destroy(armour_planner* p) {
     delete p;
 }
 
-int armour_num_constraints(const armour_planner* p, int O) { return p ? NF * p->T + p->T * p->NJ * O + NF * 4 : ARMOUR_E_ARG; }
+int armour_num_constraints(const armour_planner* p, int O) { return p ? p->d.nt + p->T * p->NJ * O + NF * 4 : ARMOUR_E_ARG; }
 int armour_num_joints(const armour_planner* p) { return p ? p->NJ : ARMOUR_E_ARG; }
 
 int armour_get_joint_bounds(const armour_planner* p, double* b) {
@@ -731,13 +790,41 @@ int armour_get_joint_bounds(const armour_planner* p, double* b) {
     return 0;
 }
 
+static int reach_uploaded(armour_planner* p, armour_timing* timing, std::chrono::steady_clock::time_point t0);
+static int plan_uploaded(armour_planner* p, armour_result* results, armour_timing* timing,
+                         std::chrono::steady_clock::time_point t0);
+
 int armour_reach_batch(armour_planner* p, int W, const armour_world* worlds, armour_timing* timing) {
+    DeviceScope device_scope(p);
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    if (p->armtd) return fail(ARMOUR_E_ARG, "an ARMTD planner takes armour_armtd_world (armour_reach_armtd_batch)");
+    p->reached = p->planned = false;
+    auto t0 = std::chrono::steady_clock::now();
+    const int rc = upload_worlds(p, W, worlds);
+    return rc ? rc : reach_uploaded(p, timing, t0);
+}
+
+int armour_reach_armtd_batch(armour_planner* p, int W, const armour_armtd_world* worlds, armour_timing* timing) {
     DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     p->reached = p->planned = false;
     auto t0 = std::chrono::steady_clock::now();
-    int rc = upload_worlds(p, W, worlds);
-    if (rc) return rc;
+    const int rc = upload_armtd(p, W, worlds);
+    return rc ? rc : reach_uploaded(p, timing, t0);
+}
+
+int armour_plan_armtd_batch(armour_planner* p, int W, const armour_armtd_world* worlds, armour_result* results,
+                            armour_timing* timing) {
+    DeviceScope device_scope(p);
+    if (!p || !results) return fail(ARMOUR_E_ARG, "null planner / results");
+    p->reached = p->planned = false;
+    auto t0 = std::chrono::steady_clock::now();
+    const int rc = upload_armtd(p, W, worlds);
+    return rc ? rc : plan_uploaded(p, results, timing, t0);
+}
+
+static int reach_uploaded(armour_planner* p, armour_timing* timing, std::chrono::steady_clock::time_point t0) {
+    int rc = 0;
     HIPCK(hipEventRecord(p->ev[0], p->stream));
     if ((rc = run_reach(p))) return rc;
     HIPCK(hipEventRecord(p->ev[1], p->stream));
@@ -757,10 +844,17 @@ int armour_reach_batch(armour_planner* p, int W, const armour_world* worlds, arm
 int armour_plan_batch(armour_planner* p, int W, const armour_world* worlds, armour_result* results, armour_timing* timing) {
     DeviceScope device_scope(p);
     if (!p || !results) return fail(ARMOUR_E_ARG, "null planner / results");
+    if (p->armtd) return fail(ARMOUR_E_ARG, "an ARMTD planner takes armour_armtd_world (armour_plan_armtd_batch)");
     p->reached = p->planned = false;
     auto t0 = std::chrono::steady_clock::now();
-    int rc = upload_worlds(p, W, worlds);
-    if (rc) return rc;
+    const int rc = upload_worlds(p, W, worlds);
+    return rc ? rc : plan_uploaded(p, results, timing, t0);
+}
+
+static int plan_uploaded(armour_planner* p, armour_result* results, armour_timing* timing,
+                         std::chrono::steady_clock::time_point t0) {
+    int rc = 0;
+    const int W = p->W;
     HIPCK(hipEventRecord(p->ev[0], p->stream));
     if ((rc = run_reach(p))) return rc;
     HIPCK(hipEventRecord(p->ev[1], p->stream));

@@ -790,14 +790,16 @@ struct ProgramBuilder {
     }
 
     // the whole job, op for op KPR/Trajectory.cu:63-254, Dynamics.cu:69-181, armour_main.cu:118-211
-    void build(const RobotParams& rp) {
+    // fk_only: the ARMTD comparison planner's program (ACMP/armtd_main.cu:141-156): joint
+    // rotations, forward kinematics and reduce_link_PZ; no velocity PZs, no RNEA, no torque
+    void build(const RobotParams& rp, bool fk_only = false) {
         this->rp = &rp;
         const int NJ = rp.num_joints;
         int R[MAX_J + 1], RT[MAX_J], QD[NF], QDA[NF], QDD[NF];
         emit(OP_JRS);
         // ops of one kind that do not depend on each other are emitted back to back, so that
         // group() can run them lane-parallel
-        for (int i = 0; i < NF; i++) {
+        for (int i = 0; i < NF && !fk_only; i++) {
             QD[i] = out(OP_MAKE1D, 0, 0, 0, i);
             QDA[i] = out(OP_MAKE1D, 0, 1, 0, i);
             QDD[i] = out(OP_MAKE1D, 0, 2, 0, i);
@@ -813,8 +815,10 @@ struct ProgramBuilder {
             }
         }
         for (int i = NF; i < NJ; i++) R[i] = cnst(CONST_RPY, i);
-        for (int i = 0; i < NJ; i++) RT[i] = out(OP_TRANSPOSE, R[i]);
-        R[NJ] = cnst(CONST_RPY, MAX_J);  // PZsparse(0, 0, 0)
+        if (!fk_only) {
+            for (int i = 0; i < NJ; i++) RT[i] = out(OP_TRANSPOSE, R[i]);
+            R[NJ] = cnst(CONST_RPY, MAX_J);  // PZsparse(0, 0, 0)
+        }
 
         // forward kinematics (Dynamics.cu:69-81) + reduce_link_PZ (armour_main.cu:124-126)
         {
@@ -836,6 +840,10 @@ struct ProgramBuilder {
             rel({FKR, FKT});
             for (int i = 0; i < NJ; i++) emit(OP_EMIT_LINK, -1, links[i], 0, 0, i);
             for (int i = 0; i < NJ; i++) rel(links[i]);
+        }
+        if (fk_only) {
+            finish();
+            return;
         }
 
         // RNEA, nominal and interval fused (Dynamics.cu:83-181)
@@ -942,6 +950,9 @@ struct ProgramBuilder {
         for (int i = NJ - 1; i >= 0; i--)
             if (us[i] >= 0) rel(us[i]);
         emit(OP_TORQUE_RADIUS);
+        finish();
+    }
+    void finish() {
         // thread-0 ops chained back to back need no barrier between them
         auto t0_only = [](int c) {
             return c == OP_MAKE1D || c == OP_MAKEROT || c == OP_MAKEBOX || c == OP_CONST || c == OP_ZERO ||

@@ -35,6 +35,31 @@ __global__ void jrs_kernel(const RobotParams* __restrict__ rpp, int W, int T, co
     }
 }
 
+// ARMTD comparison planner (ACMP/Trajectory.cu:29-72): the offline JRS tables of cos / sin of the
+// relative joint angle rotated by q0, as the JRS scalars the reach program's MAKEROT reads (the
+// k-generator and the radius of the cos / sin 1-D PZs; radius x 5 as :43, :56). tables:
+// [W][NF][6][T] = c_cos, g_cos, r_cos, c_sin, g_sin, r_sin (armtd_main.cu:70-90)
+__global__ void jrs_armtd_kernel(int W, int T, const double* q0, const double* tables, JrsJoint* out) {
+    const long n = (long)W * T * NF;
+    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(idx % NF);
+        const long j = idx / NF;
+        const int t = (int)(j % T), w = (int)(j / T);
+        const double* tb = tables + ((long)w * NF + i) * 6 * T;
+        const double c_cos = tb[0 * T + t], g_cos = tb[1 * T + t], r_cos = tb[2 * T + t];
+        const double c_sin = tb[3 * T + t], g_sin = tb[4 * T + t], r_sin = tb[5 * T + t];
+        const double cq = cos(q0[w * NF + i]), sq = sin(q0[w * NF + i]);
+        JrsJoint J = {};
+        J.cos_c = cq * c_cos - sq * c_sin;
+        J.cos_k = cq * g_cos - sq * g_sin;
+        J.cos_e = (fabs(cq) * r_cos + fabs(sq) * r_sin) * 5.0;
+        J.sin_c = cq * c_sin + sq * c_cos;
+        J.sin_k = cq * g_sin + sq * g_cos;
+        J.sin_e = (fabs(cq) * r_sin + fabs(sq) * r_cos) * 5.0;
+        out[idx] = J;
+    }
+}
+
 struct ReachArgs {
     int W, T;
     const JrsJoint* jrs;  // [W][T][NF] from jrs_kernel

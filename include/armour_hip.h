@@ -120,13 +120,36 @@ int armour_robot_builtin(int robot_id, armour_robot* out);
 armour_planner* armour_create_robot(const armour_config* cfg, const armour_robot* robot);
 const char* armour_last_error(void);
 
-/* constraints of a world with O obstacles: 7T + 7*T*O + 28  (KPR/NLPclass.cu:47-49) */
+/* constraints of a world with O obstacles: 7T + NJ*T*O + 28 (KPR/NLPclass.cu:47-49); ARMTD
+ * planners NJ*T*O + 28 (ACMP/NLPclass.cu:45-46) */
 int armour_num_constraints(const armour_planner* p, int num_obstacles);
 
 /* Plan a batch (all worlds must carry the same number of obstacles). Replaces
  * armour_main.cu:87-316 for each world. */
 int armour_plan_batch(armour_planner* p, int num_worlds, const armour_world* worlds, armour_result* results,
                       armour_timing* timing);
+
+/* The ARMTD comparison planner (kinova_planner_realtime_armtd_comparison/, "ACMP/"): the content
+ * of one armtd.in (ACMP/armtd_main.cu:37-102). Joint rotations come from offline JRS tables that the
+ * caller slices (KSI/uarmtd_planner.m:260-318) instead of the Bernstein trajectory; the plan keeps
+ * forward kinematics and collision avoidance (no RNEA, no torque rows), with the constant-
+ * acceleration joint extrema and cost of ACMP/Trajectory.cu:83-383, ACMP/NLPclass.cu:186-246. */
+typedef struct armour_armtd_world {
+    double q0[ARMOUR_NUM_FACTORS];
+    double qd0[ARMOUR_NUM_FACTORS];
+    double q_des[ARMOUR_NUM_FACTORS];
+    const double* jrs_tables;  /* [7][6][num_time_steps]: per joint c_cos, g_cos, r_cos, c_sin, g_sin, r_sin */
+    double k_range[ARMOUR_NUM_FACTORS];
+    int num_obstacles;
+    const double* obstacles;   /* [num_obstacles][12] */
+} armour_armtd_world;
+
+/* an ARMTD planner (the reference's NUM_TIME_STEPS is 100, ACMP/Parameters.h:17; solver tolerance
+ * 1e-7, :42); armour_num_constraints gives 7*T*O + 28, the getters work as for armour_create */
+armour_planner* armour_create_armtd(const armour_config* cfg);
+int armour_plan_armtd_batch(armour_planner* p, int num_worlds, const armour_armtd_world* worlds,
+                            armour_result* results, armour_timing* timing);
+int armour_reach_armtd_batch(armour_planner* p, int num_worlds, const armour_armtd_world* worlds, armour_timing* timing);
 
 /* Reach-set half only (armour_main.cu:87-222) for a batch; enables armour_eval_constraints. */
 int armour_reach_batch(armour_planner* p, int num_worlds, const armour_world* worlds, armour_timing* timing);

@@ -33,6 +33,8 @@ def lib():
         L.oracle_create_robot.restype = ctypes.c_void_p
         L.oracle_create_robot.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [_dp] * 5 + [ctypes.c_int]
         L.oracle_free.argtypes = [ctypes.c_void_p]
+        L.oracle_create_armtd.restype = ctypes.c_void_p
+        L.oracle_create_armtd.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int] + [_dp] * 6 + [ctypes.c_int]
         L.oracle_reach.restype = ctypes.c_double
         L.oracle_reach.argtypes = [ctypes.c_void_p]
         L.oracle_num_constraints.argtypes = [ctypes.c_void_p]
@@ -162,3 +164,25 @@ class OraclePlanner:
         return dict(k_opt=k, feasible=bool(feas), g=g, reach_ms=stats[0], nlp_ms=stats[1],
                     iterations=int(stats[2]), evaluations=int(stats[3]), status=int(stats[4]),
                     cost=stats[5], kkt=stats[6])
+
+
+class OracleArmtd(OraclePlanner):
+    """The ARMTD comparison planner (oracle/src/armtd.h) on one problem: the content of armtd.in
+    (ACMP/armtd_main.cu:37-102). tables: [7][6][T] = c_cos, g_cos, r_cos, c_sin, g_sin, r_sin."""
+
+    def __init__(self, q0, qd0, q_des, tables, k_range, obstacles, T=100, threads=1):
+        self.T = T
+        self.NJ = 7
+        obstacles = np.ascontiguousarray(np.asarray(obstacles, dtype=np.float64).reshape(-1, 12))
+        self.O = obstacles.shape[0]
+        arrs = [np.ascontiguousarray(np.asarray(a, dtype=np.float64)) for a in (q0, qd0, q_des)]
+        tab = np.ascontiguousarray(np.asarray(tables, dtype=np.float64).reshape(7, 6, T))
+        kr = np.ascontiguousarray(np.asarray(k_range, dtype=np.float64))
+        obs = obstacles if self.O > 0 else np.zeros((1, 12))
+        self._keep = (arrs, tab, kr, obs)
+        self.h = lib().oracle_create_armtd(None, T, self.O, *[_ptr(a) for a in arrs], _ptr(tab), _ptr(kr), _ptr(obs),
+                                           threads)
+        if not self.h:
+            raise ValueError("oracle_create_armtd failed")
+        self.m = lib().oracle_num_constraints(self.h)
+        self.reach_ms = None

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <vector>
 #include "ipm.h"
+#include "armtd.h"
 #include "planner.h"
 
 using namespace oracle;
@@ -123,6 +124,21 @@ void* oracle_create_robot(const void* robot, int T, int O, const double* q0, con
     }
 }
 
+// the ARMTD comparison planner (armtd.h): tables [joint][6][T] = c_cos, g_cos, r_cos, c_sin,
+// g_sin, r_sin (ACMP/armtd_main.cu:70-90), k_range [7]; robot: null (Kinova) or a RobotDesc
+void* oracle_create_armtd(const void* robot, int T, int O, const double* q0, const double* qd0, const double* q_des,
+                          const double* tables, const double* k_range, const double* obstacles, int threads) {
+    try {
+        Robot r = robot ? robot_from_desc(*static_cast<const RobotDesc*>(robot)) : robot_by_id(0);
+        Params p = default_params(T);
+        Planner* P = new ArmtdPlanner(r, p, q0, qd0, q_des, tables, k_range, O, obstacles);
+        P->num_threads = threads > 0 ? threads : 1;
+        return P;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
 void oracle_free(void* h) { delete static_cast<Planner*>(h); }
 
 // runs the reach-set half of a plan (armour_main.cu:97-222); returns elapsed ms or -1
@@ -225,6 +241,7 @@ int oracle_plan(void* h, double* k_opt, double* g_out, double* stats, int max_it
     auto t1 = std::chrono::high_resolution_clock::now();
     PlannerNlp nlp(P);
     IpmOptions opt;
+    opt.tol = P->tol;
     if (max_iter > 0) opt.max_iter = max_iter;
     double x[NF] = {0, 0, 0, 0, 0, 0, 0};  // NLPclass.cu:193-199
     std::vector<double> g(P->m());

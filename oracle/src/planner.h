@@ -26,21 +26,23 @@ struct Planner {
     std::vector<double> hA, hd, hdelta;  // hyperplanes [((t*NJ + l)*O + o)*COMB + p] (CollisionChecking.cu:283-295)
     int num_threads = 1;
 
+    double tol = 1e-4;                // the solver's tolerance (IPOPT_OPTIMIZATION_TOLERANCE, Parameters.h:50)
+
     Planner(const Robot& r, const Params& p, const double* q0, const double* qd0, const double* qdd0,
             const double* q_des, int num_obstacles, const double* obs);
-    ~Planner();
+    virtual ~Planner();
 
-    void reach();                     // armour_main.cu:97-222
+    virtual void reach();             // armour_main.cu:97-222
     void buffer_obstacles();          // CollisionChecking.cu:136-228 (part of reach())
     // test tooling: replace the obstacle set after reach() (the reach sets do not depend on it)
     void set_obstacles(int num_obstacles, const double* obs);
-    int m() const { return NF * T + NJ * T * O + NF * 4; }  // NLPclass.cu:47-49
-    void bounds(double* g_l, double* g_u) const;              // NLPclass.cu:87-165
-    double eval_f(const double* x) const;                     // :207-236
-    void eval_grad_f(const double* x, double* grad) const;    // :241-267
+    virtual int m() const { return NF * T + NJ * T * O + NF * 4; }  // NLPclass.cu:47-49
+    virtual void bounds(double* g_l, double* g_u) const;              // NLPclass.cu:87-165
+    virtual double eval_f(const double* x) const;                     // :207-236
+    virtual void eval_grad_f(const double* x, double* grad) const;    // :241-267
     // eval_g and eval_jac_g (:272-396); jac may be null; also returns sliced link centres
-    void eval_g_jac(const double* x, double* g, double* jac, double* link_center = nullptr) const;
-    bool feasible(const double* g) const;                     // :449-538
+    virtual void eval_g_jac(const double* x, double* g, double* jac, double* link_center = nullptr) const;
+    virtual bool feasible(const double* g) const;                     // :449-538
 
     // pieces exposed for parity tests
     void link_slice(int t, int l, const double* x, double* c3, double* grad21) const;

@@ -40,9 +40,11 @@ DEBUG_QD0 = np.array([1.0, 1.0, 1.0, -1.0, -1.0, -1.0, -1.0])     # :30
 DEBUG_QDD0 = np.full(7, 2.0)                                       # :31
 
 
-def collision_slice(T, NJ, O):
-    """rows of the collision block g[7T + (l*T + t)*O + o] (NLPclass.cu:290-296)"""
-    return slice(7 * T, 7 * T + NJ * T * O)
+def collision_slice(T, NJ, O, nt=None):
+    """rows of the collision block g[nt + (l*T + t)*O + o] (NLPclass.cu:290-296); nt = 7T torque rows
+    before it (ARMTD, ACMP/NLPclass.cu:273: none)"""
+    nt = 7 * T if nt is None else nt
+    return slice(nt, nt + NJ * T * O)
 
 
 def start_state(rng, kind, robot=KINOVA):
@@ -65,13 +67,13 @@ def _box(c, half):
     return np.concatenate([c, np.diag(half).T.reshape(-1)])
 
 
-def _obstacle_max(R, obs, x0, T, NJ):
+def _obstacle_max(R, obs, x0, T, NJ, nt=None):
     R.set_obstacles(obs[None, :])
     g = R.eval(x0, jac=False)
-    return g[collision_slice(T, NJ, 1)].max()
+    return g[collision_slice(T, NJ, 1, nt)].max()
 
 
-def tune_obstacle(R, rng, lc, x0, T, NJ, target, t_lo=0.3):
+def tune_obstacle(R, rng, lc, x0, T, NJ, target, t_lo=0.3, nt=None):
     """box obstacle whose largest collision value at x0 is `target` (to ~1e-7): centre on a ray from
     a link centre lc[t, l] (t in [t_lo, 1) of the plan), distance found by bisection."""
     for _ in range(20):
@@ -82,13 +84,13 @@ def tune_obstacle(R, rng, lc, x0, T, NJ, target, t_lo=0.3):
         u /= np.linalg.norm(u)
         base = lc[t, l]
         lo, hi = 0.0, 1.5
-        if _obstacle_max(R, _box(base + u * hi, half), x0, T, NJ) >= target:
+        if _obstacle_max(R, _box(base + u * hi, half), x0, T, NJ, nt) >= target:
             continue
-        if _obstacle_max(R, _box(base + u * lo, half), x0, T, NJ) <= target:
+        if _obstacle_max(R, _box(base + u * lo, half), x0, T, NJ, nt) <= target:
             continue
         for _ in range(48):
             mid = 0.5 * (lo + hi)
-            if _obstacle_max(R, _box(base + u * mid, half), x0, T, NJ) > target:
+            if _obstacle_max(R, _box(base + u * mid, half), x0, T, NJ, nt) > target:
                 lo = mid
             else:
                 hi = mid
@@ -131,6 +133,6 @@ def boundary_world(seed, kind, T, O, threads=8, robot=KINOVA, n_tuned=None, t_lo
     return (q0, qd0, qdd0, q_des, obstacles), x0
 
 
-def near_threshold_rows(g, T, NJ, O, band=1e-3):
-    col = g[collision_slice(T, NJ, O)]
+def near_threshold_rows(g, T, NJ, O, band=1e-3, nt=None):
+    col = g[collision_slice(T, NJ, O, nt)]
     return int(np.sum(np.abs(col - COL_THR) < band))
