@@ -672,9 +672,19 @@ int armour_device_compute_units(int device) {
     return n;
 }
 
-// streaming copy, 16 B per lane per access, grid-stride (the achievable-HBM reference kernel)
+// streaming copy, 16 B per lane per access, four independent loads in flight per lane, grid-stride
+// (the achievable-HBM reference kernel)
 __global__ __launch_bounds__(256) void copy_kernel(const double2* __restrict__ src, double2* __restrict__ dst, long n) {
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) dst[i] = src[i];
+    const long stride = (long)gridDim.x * blockDim.x;
+    long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const double2 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
 }
 
 double armour_copy_bandwidth(int device, size_t bytes, int reps) {

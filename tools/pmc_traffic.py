@@ -26,6 +26,7 @@ def main():
     fpath, wpath, kernel, out = sys.argv[1:5]
     rnd = sys.argv[5] if len(sys.argv) > 5 else "r01"
     batch = int(sys.argv[6]) if len(sys.argv) > 6 else 327  # bench.py's default on MI355X (256 CUs, T=100)
+    profile = sys.argv[7] if len(sys.argv) > 7 else "default"  # world profile of the measured batch
     fetch = per_dispatch(fpath, "FETCH_SIZE", kernel)
     write = per_dispatch(wpath, "WRITE_SIZE", kernel)
     if not fetch or not write:
@@ -35,8 +36,9 @@ def main():
     res = dict(kernel=kernel, launches=[len(fetch), len(write)], fetch_size_kib=f_kib, write_size_kib=w_kib,
                traffic_bytes_per_launch=(2 * f_kib + w_kib) * 1024,
                correction="bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM)",
-               config=dict(T=100, O=20, batch=batch), round=rnd,
-               command="rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE --output-format csv -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0")
+               config=dict(T=100, O=20, batch=batch), profile=profile, round=rnd,
+               command="rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE --output-format csv -- python3 bench.py --planners 1 "
+                       "--steps 1 --warmup 0 --cpu-seconds 0 --no-extras")
     import hashlib
     import os
 
