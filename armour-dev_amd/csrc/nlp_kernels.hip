@@ -308,7 +308,9 @@ __device__ __noinline__ void armtd_extrema_cost(const NlpDev& d, int w, const do
 // armour_eval_constraints); mode 1: the line-search trial ws.xt into the non-current slot (worlds
 // still searching only). The sliced link centres go to the slot's own region (feasible_kernel
 // copies the current slot's, the final iterate's, out).
-template <typename R>
+// ARMTD selects the comparison planner's extrema and cost at compile time: a call into them from
+// the ARMOUR instantiation would cost it registers and a stack frame (occupancy 4 -> 3 waves/SIMD)
+template <typename R, bool ARMTD>
 __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
     // mode 3: speculative trial k of list entry i (blockIdx.y = i * K + k) into its own slot
     if (mode == 1 && d.lcount && blockIdx.y >= *d.lcount) return;
@@ -442,8 +444,8 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         }
       }
     }
-    if (tid == blockDim.x - 1 && t == 0 && d.armtd) {
-        armtd_extrema_cost(d, w, x, Gb, Jb, fb, gradb);
+    if constexpr (ARMTD) {
+        if (tid == blockDim.x - 1 && t == 0) armtd_extrema_cost(d, w, x, Gb, Jb, fb, gradb);
     } else if (tid == blockDim.x - 1 && t == 0) {
         // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267)
         const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
@@ -658,8 +660,10 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
 // the product evaluation is fp64; eval_kernel_t<float> serves only the fp32 tolerance study
 // (ARMOUR_EVAL_F32, tools/fp32_study.py): reach sets stay fp64, the slicing and collision
 // arithmetic runs in float
-template __global__ void eval_kernel_t<double>(NlpDev, int);
-template __global__ void eval_kernel_t<float>(NlpDev, int);
+template __global__ void eval_kernel_t<double, false>(NlpDev, int);
+template __global__ void eval_kernel_t<float, false>(NlpDev, int);
+template __global__ void eval_kernel_t<double, true>(NlpDev, int);
+template __global__ void eval_kernel_t<float, true>(NlpDev, int);
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM

@@ -557,9 +557,11 @@ static int nside_count(const armour_planner* p) {
 }
 
 // g and J of every world of the batch (eval_kernel_t): fp64, or float for the tolerance study
-static void launch_eval(armour_planner* p, dim3 grid, int mode) {
-    if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, grid, dim3(EVAL_THREADS), 0, p->stream, p->d, mode);
-    else hipLaunchKernelGGL(eval_kernel_t<double>, grid, dim3(EVAL_THREADS), 0, p->stream, p->d, mode);
+// (the ARMTD planner's extrema and cost in their own instantiation)
+static void launch_eval(armour_planner* p, dim3 grid, const NlpDev& d, int mode) {
+    auto k = p->eval_f32 ? (d.armtd ? eval_kernel_t<float, true> : eval_kernel_t<float, false>)
+                         : (d.armtd ? eval_kernel_t<double, true> : eval_kernel_t<double, false>);
+    hipLaunchKernelGGL(k, grid, dim3(EVAL_THREADS), 0, p->stream, d, mode);
 }
 
 static int run_solver(armour_planner* p) {
@@ -571,7 +573,7 @@ static int run_solver(armour_planner* p) {
     d.wl_run = Li[0];
     d.ls0 = 0;
     hipLaunchKernelGGL(ipm_world_init, dim3((W + 63) / 64), dim3(64), 0, p->stream, d);
-    launch_eval(p, dim3(p->T, W), 0);
+    launch_eval(p, dim3(p->T, W), d, 0);
     hipLaunchKernelGGL(ipm_rows_init, dim3(d.nblk, W), dim3(ROW_THREADS), 0, p->stream, d);
     HIPCK(hipGetLastError());
     const int ns = nside_count(p);
@@ -601,8 +603,7 @@ static int run_solver(armour_planner* p) {
             dc.wl_search = Ls[1];
             dc.ls0 = 1;
             dc.lcount_out = d.cnt + 5;
-            if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, dim3(p->T, nrun), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
-            else hipLaunchKernelGGL(eval_kernel_t<double>, dim3(p->T, nrun), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
+            launch_eval(p, dim3(p->T, nrun), dc, 1);
             hipLaunchKernelGGL(ipm_rows_C, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, dc);
             hipLaunchKernelGGL(ipm_world_C, dim3(nrun), dim3(64), 0, p->stream, dc);
             HIPCK(hipStreamSynchronize(p->stream));
@@ -613,8 +614,7 @@ static int run_solver(armour_planner* p) {
             NlpDev ds = d;
             ds.wl = Ls[1];
             const int ny = nsearch * d.K;
-            if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, dim3(p->T, ny), dim3(EVAL_THREADS), 0, p->stream, ds, 3);
-            else hipLaunchKernelGGL(eval_kernel_t<double>, dim3(p->T, ny), dim3(EVAL_THREADS), 0, p->stream, ds, 3);
+            launch_eval(p, dim3(p->T, ny), ds, 3);
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, ny), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nsearch), dim3(64), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_copy_spec, dim3(64, nsearch), dim3(256), 0, p->stream, ds);
@@ -626,8 +626,7 @@ static int run_solver(armour_planner* p) {
                 dc.wl_search = Ls[(ls + 1) & 1];
                 dc.lcount_out = d.cnt + 4 + ((ls + 1) & 1);
                 dc.ls0 = 0;
-                if (p->eval_f32) hipLaunchKernelGGL(eval_kernel_t<float>, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
-                else hipLaunchKernelGGL(eval_kernel_t<double>, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, dc, 1);
+                launch_eval(p, dim3(p->T, nsearch), dc, 1);
                 hipLaunchKernelGGL(ipm_rows_C, dim3(d.nblk, nsearch), dim3(ROW_THREADS), 0, p->stream, dc);
                 hipLaunchKernelGGL(ipm_world_C, dim3(nsearch), dim3(64), 0, p->stream, dc);
             }
@@ -922,7 +921,7 @@ int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g
         ws[i].cur = 0;
     }
     HIPCK(hipMemcpyAsync(d.ws, ws.data(), sizeof(WorldState) * p->W, hipMemcpyHostToDevice, p->stream));
-    launch_eval(p, dim3(p->T, p->W), 0);
+    launch_eval(p, dim3(p->T, p->W), d, 0);
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(g, d.g + gidx(d, 0, w, 0), sizeof(double) * d.m, hipMemcpyDeviceToHost, p->stream));
     if (jac) HIPCK(hipMemcpyAsync(jac, d.J + gidx(d, 0, w, 0) * NF, sizeof(double) * d.m * NF, hipMemcpyDeviceToHost, p->stream));
