@@ -137,6 +137,73 @@ __device__ inline __attribute__((always_inline)) void mixed_plane(const R* ga, c
         if (f != E) del += fabs(C[f] * G[BUF_GEN - 3 + f][f]);
 }
 
+// mixed plane of obstacle generator ga and link generator j (0..2 box, 3..5 the radii): the
+// mixed_plane<E> specialisation for j (folds to one call once j is a constant)
+template <typename R>
+__device__ inline __attribute__((always_inline)) void mixed_plane_j(int j, const R* ga, const R (*G)[3], const R* oc,
+                                                                    R* C, R& dd, R& del) {
+    switch (j) {
+        case 3: mixed_plane<0>(ga, G[OBS_GEN + 3], G, oc, C, dd, del); break;
+        case 4: mixed_plane<1>(ga, G[OBS_GEN + 4], G, oc, C, dd, del); break;
+        case 5: mixed_plane<2>(ga, G[OBS_GEN + 5], G, oc, C, dd, del); break;
+        default: mixed_plane<-1>(ga, G[OBS_GEN + j], G, oc, C, dd, del); break;
+    }
+}
+
+// table entry of link-link plane p (generators i < j of the link's 6): the normal, A . c (c: the
+// sliced centre in the evaluation, the centre of its range in the cache build) and |A . g_k| of the
+// link's 6 generators (the link's part of delta, kept per summand for the reference's order)
+template <typename R>
+__device__ inline __attribute__((always_inline)) void ll_table(const R* lg, int p, const R* c, R* P) {
+    int i = 0, rem = p;
+    while (rem >= 5 - i) { rem -= 5 - i; i++; }
+    const int j = i + 1 + rem;
+    R A0, A1, A2;
+    plane_normal(lg + 3 * i, lg + 3 * j, A0, A1, A2);
+    P[0] = A0; P[1] = A1; P[2] = A2;
+    P[3] = A0 * c[0] + A1 * c[1] + A2 * c[2];
+#pragma unroll
+    for (int k = 0; k < 6; k++) P[4 + k] = fabs(A0 * lg[3 * k] + A1 * lg[3 * k + 1] + A2 * lg[3 * k + 2]);
+}
+// table entry of obstacle-obstacle plane p: the normal, d = A . c_obs and the obstacle's part of delta
+template <typename R>
+__device__ inline __attribute__((always_inline)) void oo_table(const R* ob, int p, R* P) {
+    const int i = p == 2 ? 1 : 0, j = p == 0 ? 1 : 2;
+    R A0, A1, A2;
+    plane_normal(ob + 3 * (i + 1), ob + 3 * (j + 1), A0, A1, A2);
+    P[0] = A0; P[1] = A1; P[2] = A2;
+    P[3] = A0 * ob[0] + A1 * ob[1] + A2 * ob[2];
+    R del = 0.0;
+#pragma unroll
+    for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * ob[3 * (k + 1)] + A1 * ob[3 * (k + 1) + 1] + A2 * ob[3 * (k + 1) + 2]);
+    P[4] = del;
+}
+// d and delta of a link-link plane for one obstacle (generators G[0..2], centre oc), delta summed
+// in the reference's order: the obstacle's generators first, then the link's
+template <typename R>
+__device__ inline __attribute__((always_inline)) void ll_complete(const R* P, const R (*G)[3], const R* oc, R& dd, R& del) {
+    const R A0 = P[0], A1 = P[1], A2 = P[2];
+    dd = A0 * oc[0] + A1 * oc[1] + A2 * oc[2];
+    del = 0.0;
+#pragma unroll
+    for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
+#pragma unroll
+    for (int k = 0; k < 6; k++) del += P[4 + k];
+}
+// d and delta of an obstacle-obstacle plane for one link (generators L[0..2], radii L[3..5] on
+// axes 0..2: their products with the other components are exact zeros and dropped)
+template <typename R>
+__device__ inline __attribute__((always_inline)) void oo_complete(const R* P, const R (*L)[3], R& dd, R& del) {
+    const R A0 = P[0], A1 = P[1], A2 = P[2];
+    dd = P[3];
+    del = P[4];
+#pragma unroll
+    for (int k = 0; k < 3; k++) del += fabs(A0 * L[k][0] + A1 * L[k][1] + A2 * L[k][2]);
+    del += fabs(A0 * L[3][0]);
+    del += fabs(A1 * L[4][1]);
+    del += fabs(A2 * L[5][2]);
+}
+
 // one monomial's contribution to a slice (k = 0) or to its derivative in x_{k-1}: the products
 // of PZsparse.cu:404-435 / 477-516 in factor order, v * 1.0 standing in for a skipped factor
 // ptab[j][g] = x_j^g (g = 0: 1.0, the skipped factor exactly), ptab[j][4 + g] = g x_j^(g-1): one
@@ -300,6 +367,200 @@ __device__ __noinline__ void armtd_extrema_cost(const NlpDev& d, int w, const do
         const double dk = kr[i] * 0.125;
         const double gv = rp.wrap_mask[i] ? (2 * wrap_to_pi(qp[i] - d.qdes[w * NF + i]) * dk) : (2 * (qp[i] - d.qdes[w * NF + i]) * dk);
         gradb[i] = gv * rp.cost_scale;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Certified plane cache, grid (T, W), once per reach. The collision value of
+// a (link, obstacle) pair is max over the 36 planes of the buffered obstacle of
+// max(A . c - (d + delta), -A . c - (-d + delta)) (CollisionChecking.cu:230-299), where A, d and
+// delta depend on the reach sets and the obstacle only and c = c(x) is the sliced link centre.
+// Over the box |x_i| <= PC_XBOX, c(x) lies in centre +- rad (rad = sum of |coefficient| of the
+// link's k-monomials, times PC_RADF), which bounds each candidate between lo and hi. With M the
+// largest lo, a plane whose hi < M - PC_MARGIN is below the maximum for every x in the box, by far
+// more than the rounding of the evaluation: the scan over the remaining planes, in the reference's
+// order with the same arithmetic, returns the same value, the same winning plane and the same
+// first-maximum tie-break. Those planes are stored (A, d + delta, -d + delta) for eval_kernel.
+__device__ inline __attribute__((always_inline)) void pc_bounds(const double* A, double P, double N, const double* cen,
+                                                                const double* rad, double& lo, double& hi) {
+    const double Ac = A[0] * cen[0] + A[1] * cen[1] + A[2] * cen[2];
+    const double S = fabs(A[0]) * rad[0] + fabs(A[1]) * rad[1] + fabs(A[2]) * rad[2];
+    lo = fmax(Ac - S - P, -Ac - S - N);
+    hi = fmax(Ac + S - P, -Ac + S - N);
+}
+__device__ inline bool nonzero3(const double* A) { return A[0] != 0 || A[1] != 0 || A[2] != 0; }
+
+__global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
+    const int t = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
+    const long jt = (long)w * d.T + t;
+    const int NJ = d.NJ, O = d.O, NP = NJ * O;
+    __shared__ double cen[MAX_J][3], rad[MAX_J][3];
+    __shared__ double lgen[MAX_J][18];
+    __shared__ double obs[MAX_OBS][12];
+    __shared__ double llp[MAX_J][LL_PLANES][10];
+    __shared__ double oop[MAX_OBS][OO_PLANES][5];
+    __shared__ double mixlo[MAX_J * MAX_OBS * OBS_GEN];
+    __shared__ unsigned char mixbits[MAX_J * MAX_OBS * OBS_GEN];
+    __shared__ double pairM[MAX_J * MAX_OBS];
+    __shared__ unsigned cntp[MAX_J * MAX_OBS];
+    __shared__ unsigned total_s;
+    for (int i = tid; i < NJ * 18; i += blockDim.x) lgen[i / 18][i % 18] = d.ro.link_gens[jt * NJ * 18 + i];
+    for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
+    if (tid < NJ * 3) {
+        const int l = tid / 3, e = tid % 3;
+        const long b = jt * NJ + l;
+        const int cnt = d.ro.link_cnt[b];
+        double r = 0.0;
+        for (int q = 0; q < cnt; q++) r += fabs(d.ro.link_coef[(b * CAP_LM + q) * 3 + e]);
+        cen[l][e] = d.ro.link_center[b * 3 + e];
+        rad[l][e] = r * PC_RADF;
+    }
+    __syncthreads();
+    for (int u = tid; u < NJ * LL_PLANES + O * OO_PLANES; u += blockDim.x) {
+        if (u < NJ * LL_PLANES) ll_table(lgen[u / LL_PLANES], u % LL_PLANES, cen[u / LL_PLANES], llp[u / LL_PLANES][u % LL_PLANES]);
+        else oo_table(obs[(u - NJ * LL_PLANES) / OO_PLANES], (u - NJ * LL_PLANES) % OO_PLANES,
+                      oop[(u - NJ * LL_PLANES) / OO_PLANES][(u - NJ * LL_PLANES) % OO_PLANES]);
+    }
+    const int nmix = NP * OBS_GEN;
+    // the 9 buffered generators of pair (l, o) (obstacle's 3, the link's 6) and the obstacle centre
+    auto load_gens = [&](int l, int o, double (*G)[3], double* oc) {
+#pragma unroll
+        for (int r = 0; r < 3; r++) oc[r] = obs[o][r];
+#pragma unroll
+        for (int q = 0; q < OBS_GEN; q++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[q][r] = obs[o][(q + 1) * 3 + r];
+#pragma unroll
+        for (int q = 0; q < 6; q++)
+#pragma unroll
+            for (int r = 0; r < 3; r++) G[OBS_GEN + q][r] = lgen[l][r + 3 * q];
+    };
+    // pass 1 over the mixed planes: the largest lower bound of each (link, obstacle, i) item
+    __syncthreads();
+    for (int u = tid; u < nmix; u += blockDim.x) {
+        const int l = u / (O * OBS_GEN), o = (u / OBS_GEN) % O, i = u % OBS_GEN;
+        double G[BUF_GEN][3], oc[3];
+        load_gens(l, o, G, oc);
+        double M = -1e300;
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            double A[3], dd, del, lo, hi;
+            mixed_plane_j(j, G[i], G, oc, A, dd, del);
+            pc_bounds(A, dd + del, -dd + del, cen[l], rad[l], lo, hi);
+            if (nonzero3(A)) M = fmax(M, lo);
+        }
+        mixlo[u] = M;
+    }
+    __syncthreads();
+    // pass 1 over the pairs: M, the largest lower bound over all 36 planes
+    for (int pr = tid; pr < NP; pr += blockDim.x) {
+        const int l = pr / O, o = pr % O;
+        double G[BUF_GEN][3], oc[3];
+        load_gens(l, o, G, oc);
+        double M = fmax(fmax(mixlo[pr * 3], mixlo[pr * 3 + 1]), mixlo[pr * 3 + 2]);
+#pragma unroll
+        for (int p = 0; p < OO_PLANES; p++) {
+            double dd, del, lo, hi;
+            oo_complete(oop[o][p], G + OBS_GEN, dd, del);
+            pc_bounds(oop[o][p], dd + del, -dd + del, cen[l], rad[l], lo, hi);
+            if (nonzero3(oop[o][p])) M = fmax(M, lo);
+        }
+        for (int p = 0; p < LL_PLANES; p++) {
+            double dd, del, lo, hi;
+            ll_complete(llp[l][p], G, oc, dd, del);
+            pc_bounds(llp[l][p], dd + del, -dd + del, cen[l], rad[l], lo, hi);
+            if (nonzero3(llp[l][p])) M = fmax(M, lo);
+        }
+        pairM[pr] = M;
+    }
+    __syncthreads();
+    // pass 2 over the mixed planes: which can reach M
+    for (int u = tid; u < nmix; u += blockDim.x) {
+        const int l = u / (O * OBS_GEN), o = (u / OBS_GEN) % O, i = u % OBS_GEN;
+        double G[BUF_GEN][3], oc[3];
+        load_gens(l, o, G, oc);
+        const double M = pairM[u / OBS_GEN] - PC_MARGIN;
+        unsigned bits = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            double A[3], dd, del, lo, hi;
+            mixed_plane_j(j, G[i], G, oc, A, dd, del);
+            pc_bounds(A, dd + del, -dd + del, cen[l], rad[l], lo, hi);
+            if (nonzero3(A) && hi >= M) bits |= 1u << j;
+        }
+        mixbits[u] = (unsigned char)bits;
+    }
+    __syncthreads();
+    // pass 2 over the pairs: the surviving planes in the reference's order (a < b over the 9
+    // buffered generators, CollisionChecking.cu:26-39); count, then offsets, then the records
+    auto survives = [&](int pr, int l, int o, int a, int b, const double (*G)[3], const double* oc) -> bool {
+        if (a < OBS_GEN && b >= OBS_GEN) return (mixbits[pr * OBS_GEN + a] >> (b - OBS_GEN)) & 1;
+        const double* P = b < OBS_GEN ? oop[o][a + b - 1] : llp[l][(a - OBS_GEN) * (11 - (a - OBS_GEN)) / 2 + b - a - 1];
+        double dd, del, lo, hi;
+        if (b < OBS_GEN) oo_complete(P, G + OBS_GEN, dd, del);
+        else ll_complete(P, G, oc, dd, del);
+        pc_bounds(P, dd + del, -dd + del, cen[l], rad[l], lo, hi);
+        return nonzero3(P) && hi >= pairM[pr] - PC_MARGIN;
+    };
+    for (int pr = tid; pr < NP; pr += blockDim.x) {
+        const int l = pr / O, o = pr % O;
+        double G[BUF_GEN][3], oc[3];
+        load_gens(l, o, G, oc);
+        unsigned n = 0;
+        for (int a = 0; a < BUF_GEN; a++)
+            for (int b = a + 1; b < BUF_GEN; b++) n += survives(pr, l, o, a, b, G, oc) ? 1 : 0;
+        cntp[pr] = n;
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive prefix over the pairs, one wave: lane k sums a contiguous chunk
+        const int per = (NP + 63) / 64, b0 = tid * per;
+        unsigned s = 0;
+        for (int q = b0; q < b0 + per && q < NP; q++) s += cntp[q];
+        unsigned incl = s;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const unsigned v = __shfl_up(incl, off);
+            if (tid >= off) incl += v;
+        }
+        unsigned run = incl - s;
+        for (int q = b0; q < b0 + per && q < NP; q++) {
+            const unsigned c = cntp[q];
+            cntp[q] = run;
+            run += c;
+            d.pcoff[jt * NP + q] = (run - c) << 8 | c;
+        }
+        if (tid == 63) total_s = incl;
+    }
+    __syncthreads();
+    const bool ok = total_s <= (unsigned)d.pc_cap;
+    if (tid == 0) d.pcok[jt] = ok ? 1 : 0;
+    if (!ok) return;
+    double* const rec = d.pc + jt * 5 * d.pc_cap;
+    const int cap = d.pc_cap;
+    for (int pr = tid; pr < NP; pr += blockDim.x) {
+        const int l = pr / O, o = pr % O;
+        double G[BUF_GEN][3], oc[3];
+        load_gens(l, o, G, oc);
+        unsigned q = cntp[pr];
+        for (int a = 0; a < BUF_GEN; a++)
+            for (int b = a + 1; b < BUF_GEN; b++) {
+                if (!survives(pr, l, o, a, b, G, oc)) continue;
+                double A[3], dd, del;
+                if (a < OBS_GEN && b >= OBS_GEN) {
+                    mixed_plane_j(b - OBS_GEN, G[a], G, oc, A, dd, del);
+                } else {
+                    const double* P = b < OBS_GEN ? oop[o][a + b - 1] : llp[l][(a - OBS_GEN) * (11 - (a - OBS_GEN)) / 2 + b - a - 1];
+                    A[0] = P[0]; A[1] = P[1]; A[2] = P[2];
+                    if (b < OBS_GEN) oo_complete(P, G + OBS_GEN, dd, del);
+                    else ll_complete(P, G, oc, dd, del);
+                }
+                rec[q] = A[0];
+                rec[cap + q] = A[1];
+                rec[2 * cap + q] = A[2];
+                rec[3 * cap + q] = dd + del;
+                rec[4 * cap + q] = -dd + del;
+                q++;
+            }
     }
 }
 
@@ -502,34 +763,51 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     // reference's left-to-right sum needs them in order), then the per-(link, obstacle) scan only
     // completes them.
     const long nt = d.nt;
-    const bool coll = !(d.diag & 2);
+    bool coll = !(d.diag & 2);
+    if constexpr (std::is_same<R, double>::value) {
+        // the certified plane cache (plane_cache_kernel) when it holds this block's planes and x lies in
+        // its box: the scan over the surviving planes, same order, same arithmetic
+        bool inbox = true;
+#pragma unroll
+        for (int j = 0; j < NF; j++) inbox = inbox && fabs(x[j]) <= PC_XBOX;
+        if (coll && d.pcready && inbox && d.pcok[jt]) {
+            const int NP = NJ * O;
+            const double* const rec = d.pc + jt * 5 * d.pc_cap;
+            const int cap = d.pc_cap;
+            for (int pr = tid; pr < NP; pr += blockDim.x) {
+                const int l = pr / O, o = pr % O;
+                const unsigned po = d.pcoff[jt * NP + pr];
+                const int n = po & 255, q0 = po >> 8;
+                const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
+                double best = -100000000.0, B0 = 0, B1 = 0, B2 = 0;
+                bool isneg = false;
+                for (int q = q0; q < q0 + n; q++) {
+                    const double A0 = rec[q], A1 = rec[cap + q], A2 = rec[2 * cap + q];
+                    const double P = rec[3 * cap + q], N = rec[4 * cap + q];
+                    const double Ac = A0 * c0 + A1 * c1 + A2 * c2;
+                    const double pos = Ac - P;
+                    const double neg = -Ac - N;
+                    if (pos > best) { best = pos; B0 = A0; B1 = A1; B2 = A2; isneg = false; }
+                    if (neg > best) { best = neg; B0 = A0; B1 = A1; B2 = A2; isneg = true; }
+                }
+                const long row = nt + ((long)l * d.T + t) * O + o;
+                Gb[row] = -best;
+#pragma unroll
+                for (int k = 0; k < NF; k++) {
+                    const double dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
+                    Jb[row * NF + k] = isneg ? dot : -dot;
+                }
+            }
+            coll = false;
+        }
+    }
     for (int u = tid; u < (coll ? NJ * LL_PLANES + O * OO_PLANES : 0); u += blockDim.x) {
         if (u < NJ * LL_PLANES) {
             const int l = u / LL_PLANES, p = u % LL_PLANES;
-            int i = 0, rem = p;
-            while (rem >= 5 - i) { rem -= 5 - i; i++; }
-            const int j = i + 1 + rem;
-            const R* ga = &lgen[l][3 * i];
-            const R* gb = &lgen[l][3 * j];
-            R A0, A1, A2;
-            plane_normal(ga, gb, A0, A1, A2);
-            R* P = llp[l][p];
-            P[0] = A0; P[1] = A1; P[2] = A2;
-            P[3] = A0 * lc[l][0] + A1 * lc[l][1] + A2 * lc[l][2];
-#pragma unroll
-            for (int k = 0; k < 6; k++) P[4 + k] = fabs(A0 * lgen[l][3 * k] + A1 * lgen[l][3 * k + 1] + A2 * lgen[l][3 * k + 2]);
+            ll_table(lgen[l], p, lc[l], llp[l][p]);
         } else {
             const int v = u - NJ * LL_PLANES, o = v / OO_PLANES, p = v % OO_PLANES;
-            const int i = p == 2 ? 1 : 0, j = p == 0 ? 1 : 2;
-            R A0, A1, A2;
-            plane_normal(&obs[o][3 * (i + 1)], &obs[o][3 * (j + 1)], A0, A1, A2);
-            R* P = oop[o][p];
-            P[0] = A0; P[1] = A1; P[2] = A2;
-            P[3] = A0 * obs[o][0] + A1 * obs[o][1] + A2 * obs[o][2];
-            R del = 0.0;
-#pragma unroll
-            for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * obs[o][3 * (k + 1)] + A1 * obs[o][3 * (k + 1) + 1] + A2 * obs[o][3 * (k + 1) + 2]);
-            P[4] = del;
+            oo_table(obs[o], p, oop[o][p]);
         }
     }
     // the 18 mixed planes (one obstacle generator i, one link generator j) depend on both: one item
@@ -619,23 +897,14 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
                 R A0, A1, A2, dd, del, Ac;
                 if (b < OBS_GEN) {
                     const R* P = oop[o][a + b - 1];
-                    A0 = P[0]; A1 = P[1]; A2 = P[2]; dd = P[3]; del = P[4];
-#pragma unroll
-                    for (int k = OBS_GEN; k < BUF_GEN - 3; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
-                    del += fabs(A0 * G[BUF_GEN - 3][0]);   // the radii (dot_z)
-                    del += fabs(A1 * G[BUF_GEN - 2][1]);
-                    del += fabs(A2 * G[BUF_GEN - 1][2]);
+                    A0 = P[0]; A1 = P[1]; A2 = P[2];
+                    oo_complete(P, G + OBS_GEN, dd, del);
                     Ac = A0 * c0 + A1 * c1 + A2 * c2;
                 } else {
                     const int i = a - OBS_GEN, j = b - OBS_GEN;
                     const R* P = llp[l][i * (11 - i) / 2 + j - i - 1];
                     A0 = P[0]; A1 = P[1]; A2 = P[2]; Ac = P[3];
-                    dd = A0 * oc[0] + A1 * oc[1] + A2 * oc[2];
-                    del = 0.0;
-#pragma unroll
-                    for (int k = 0; k < OBS_GEN; k++) del += fabs(A0 * G[k][0] + A1 * G[k][1] + A2 * G[k][2]);
-#pragma unroll
-                    for (int k = 0; k < 6; k++) del += P[4 + k];
+                    ll_complete(P, G, oc, dd, del);
                 }
                 // the reference skips a zero normal (norm > 0); for a normalised or zeroed A
                 // that is exactly "some component non-zero"

@@ -370,6 +370,13 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
             return rc;
     }
+    // certified plane cache: PC_AVG records per (link, obstacle) pair of every (world, t)
+    d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
+    d.pcready = 0;
+    d.pc_cap = PC_AVG * NJ * Om;
+    if (d.pcache && ((rc = p->alloc(&d.pc, jobs * 5 * (size_t)d.pc_cap)) || (rc = p->alloc(&d.pcoff, jobs * NJ * (size_t)Om)) ||
+                     (rc = p->alloc(&d.pcok, jobs))))
+        return rc;
     HIPCK(hipMemset(d.cnt, 0, 8 * sizeof(unsigned)));
     d.lcount = nullptr;
     d.lcount_out = nullptr;
@@ -416,6 +423,7 @@ static int upload_worlds(armour_planner* p, int W, const armour_world* worlds) {
     NlpDev& d = p->d;
     d.W = W;
     d.O = O;
+    d.pcready = 0;
     d.m = d.nt + p->T * p->NJ * O + NF * 4;
     d.R = d.m + NF;
     d.chunk = row_chunk();
@@ -548,7 +556,16 @@ static int run_reach(armour_planner* p) {
         g_err = buf;
     }
     p->reached = true;
+    p->d.pcready = 0;
     return 0;
+}
+
+// the certified plane cache of the current reach sets and obstacles (plane_cache_kernel)
+static void ensure_plane_cache(armour_planner* p) {
+    NlpDev& d = p->d;
+    if (!d.pcache || d.pcready || d.O == 0 || p->eval_f32) return;
+    hipLaunchKernelGGL(plane_cache_kernel, dim3(p->T, p->W), dim3(EVAL_THREADS), 0, p->stream, d);
+    d.pcready = 1;
 }
 
 static int nside_count(const armour_planner* p) {
@@ -572,6 +589,7 @@ static int run_solver(armour_planner* p) {
     d.wl = nullptr;
     d.wl_run = Li[0];
     d.ls0 = 0;
+    ensure_plane_cache(p);
     hipLaunchKernelGGL(ipm_world_init, dim3((W + 63) / 64), dim3(64), 0, p->stream, d);
     launch_eval(p, dim3(p->T, W), d, 0);
     hipLaunchKernelGGL(ipm_rows_init, dim3(d.nblk, W), dim3(ROW_THREADS), 0, p->stream, d);
@@ -921,6 +939,7 @@ int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g
         ws[i].cur = 0;
     }
     HIPCK(hipMemcpyAsync(d.ws, ws.data(), sizeof(WorldState) * p->W, hipMemcpyHostToDevice, p->stream));
+    ensure_plane_cache(p);
     launch_eval(p, dim3(p->T, p->W), d, 0);
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(g, d.g + gidx(d, 0, w, 0), sizeof(double) * d.m, hipMemcpyDeviceToHost, p->stream));

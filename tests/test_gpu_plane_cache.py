@@ -1,0 +1,85 @@
+"""The certified plane cache (plane_cache_kernel) against the full per-evaluation
+plane scan of the same library (ARMOUR_PLANE_CACHE=0): constraint values, Jacobians and whole plans
+bitwise equal, on survey worlds and on the decision-boundary fixtures, at points inside the
+certified box (cached scan) and outside it (full scan in both)."""
+import contextlib
+import os
+
+import numpy as np
+import pytest
+
+import armour_amd as A
+from conftest import engine
+from test_boundary import load, world
+
+pytestmark = pytest.mark.gpu
+
+
+@contextlib.contextmanager
+def env(name, value):
+    prev = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        yield
+    finally:
+        if prev is None:
+            os.environ.pop(name, None)
+        else:
+            os.environ[name] = prev
+
+
+def planners(T, O, W):
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    with env("ARMOUR_PLANE_CACHE", "0"):
+        Q = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    return P, Q
+
+
+def points(rng, n):
+    xs = [np.zeros(7), np.ones(7), -np.ones(7), np.array([1, -1, 1, -1, 1, -1, 1.0])]
+    xs += [rng.uniform(-1, 1, 7) for _ in range(n)]
+    xs += [rng.uniform(-1, 1, 7) * 1.5]  # outside the certified box: the full scan in both
+    return xs
+
+
+def check_eval(P, Q, worlds, rng, n=6):
+    P.reach(worlds)
+    Q.reach(worlds)
+    for x in points(rng, n):
+        for w in range(len(worlds)):
+            g, J = P.eval_constraints(w, x)
+            gq, Jq = Q.eval_constraints(w, x)
+            np.testing.assert_array_equal(g, gq)
+            np.testing.assert_array_equal(J, Jq)
+
+
+def check_plan(P, Q, worlds):
+    ra, _ = P.plan(worlds)
+    rb, _ = Q.plan(worlds)
+    for w, (a, b) in enumerate(zip(ra, rb)):
+        assert a["feasible"] == b["feasible"] and a["status"] == b["status"], w
+        assert a["iterations"] == b["iterations"] and a["evaluations"] == b["evaluations"], w
+        np.testing.assert_array_equal(a["k_opt"], b["k_opt"])
+        np.testing.assert_array_equal(P.constraints(w), Q.constraints(w))
+
+
+@pytest.mark.parametrize("eng", ["lane", "job"])
+def test_plane_cache_survey_worlds(eng):
+    T, O, W = 100, 20, 12
+    worlds = [A.make_world(1000 + s, O, profile="survey") for s in range(W)]
+    with engine(eng):
+        P, Q = planners(T, O, W)
+    rng = np.random.default_rng(7)
+    check_eval(P, Q, worlds, rng)
+    check_plan(P, Q, worlds)
+
+
+@pytest.mark.parametrize("name", ["boundary_config2_T100_O20", "boundary_config3_T200_O40"])
+def test_plane_cache_boundary(name):
+    fx = load(name)
+    T, W, O = int(fx["T"]), len(fx["kinds"]), fx["obstacles"].shape[1]
+    worlds = [world(fx, w) for w in range(W)]
+    P, Q = planners(T, O, W)
+    rng = np.random.default_rng(11)
+    check_eval(P, Q, worlds, rng, n=3)
+    check_plan(P, Q, worlds)
