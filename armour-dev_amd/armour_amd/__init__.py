@@ -99,6 +99,7 @@ def lib():
         L.armour_get_reach_occupancy.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong),
                                                  ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.armour_get_joint_bounds.argtypes = [ctypes.c_void_p, _dp]
+        L.armour_get_plane_cache_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.armour_get_reach_dump.argtypes = [ctypes.c_void_p, _dp, ctypes.c_int]
         L.armour_get_reach_profile.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
         for name in ("armour_get_constraints", "armour_get_link_centers", "armour_get_link_generators",
@@ -114,7 +115,8 @@ ABI_SYMBOLS = ["armour_copy_bandwidth", "armour_create", "armour_create_robot", 
                "armour_get_link_centers", "armour_get_link_generators", "armour_get_torque_radius",
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
                "armour_get_reach_dump", "armour_get_reach_occupancy", "armour_get_monomial_counts",
-               "armour_create_armtd", "armour_plan_armtd_batch", "armour_reach_armtd_batch"]
+               "armour_create_armtd", "armour_plan_armtd_batch", "armour_reach_armtd_batch",
+               "armour_get_plane_cache_stats"]
 
 
 def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
@@ -299,6 +301,13 @@ class Planner:
         rc = lib().armour_get_reach_occupancy(self.h, used, caps, n)
         _check(min(0, rc))
         return {k: (int(used[i]), int(caps[i])) for i, k in enumerate(self.OCCUPANCY)}
+
+    def plane_cache_stats(self):
+        """certified plane cache of the current reach sets (armour_get_plane_cache_stats)"""
+        keys = ("planes_kept", "pairs", "blocks_cached", "blocks", "max_per_pair", "records_per_block")
+        out = (ctypes.c_longlong * len(keys))()
+        _check(min(0, lib().armour_get_plane_cache_stats(self.h, out, len(keys))))
+        return {k: int(out[i]) for i, k in enumerate(keys)}
 
     def torque_radius(self, w):
         r = np.zeros((self.T, NF))

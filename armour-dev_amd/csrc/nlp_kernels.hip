@@ -676,10 +676,16 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         const long base = jt * NJ + l;
         R c = k == 0 ? d.ro.link_center[base * 3 + e] : 0.0;
         const int cnt = lcnt[l];
-        for (int q = 0; q < cnt; q++) {
-            const int h = lh[l][q];
-            c = c + slice_term(lco[l][q][e], h, k, ptab);
+        // four independent products in flight, summed in monomial order
+        int q = 0;
+        for (; q + 4 <= cnt; q += 4) {
+            const R v0 = slice_term(lco[l][q][e], lh[l][q], k, ptab);
+            const R v1 = slice_term(lco[l][q + 1][e], lh[l][q + 1], k, ptab);
+            const R v2 = slice_term(lco[l][q + 2][e], lh[l][q + 2], k, ptab);
+            const R v3 = slice_term(lco[l][q + 3][e], lh[l][q + 3], k, ptab);
+            c = c + v0; c = c + v1; c = c + v2; c = c + v3;
         }
+        for (; q < cnt; q++) c = c + slice_term(lco[l][q][e], lh[l][q], k, ptab);
         if (k == 0) {
             const R r = d.ro.link_rad[base * 3 + e];
             const R cc = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
@@ -695,7 +701,15 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         const long base = jt * NF + j;
         R c = k == 0 ? d.ro.tq_center[base] : 0.0;
         const int cnt = tcnt[j];
-        for (int q = 0; q < cnt; q++) c = c + slice_term(tco[j][q], th[j][q], k, ptab);
+        int q = 0;
+        for (; q + 4 <= cnt; q += 4) {
+            const R v0 = slice_term(tco[j][q], th[j][q], k, ptab);
+            const R v1 = slice_term(tco[j][q + 1], th[j][q + 1], k, ptab);
+            const R v2 = slice_term(tco[j][q + 2], th[j][q + 2], k, ptab);
+            const R v3 = slice_term(tco[j][q + 3], th[j][q + 3], k, ptab);
+            c = c + v0; c = c + v1; c = c + v2; c = c + v3;
+        }
+        for (; q < cnt; q++) c = c + slice_term(tco[j][q], th[j][q], k, ptab);
         const long gi = (long)t * NF + j;
         if (k == 0) {
             const R r = d.ro.tq_rad[base];
@@ -707,52 +721,54 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     }
     if constexpr (ARMTD) {
         if (tid == blockDim.x - 1 && t == 0) armtd_extrema_cost(d, w, x, Gb, Jb, fb, gradb);
-    } else if (tid == blockDim.x - 1 && t == 0) {
-        // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267)
-        const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
+    } else if (t == 0 && tid >= (int)blockDim.x - 2 * NF - 1) {
+        // extremum rows (NLPclass.cu:319-320, 390-391), one thread per (kind, joint), and the cost
+        // (NLPclass.cu:207-267) on one more thread
         const double* q0 = d.q0 + w * NF;
         const double* qd0 = d.qd0 + w * NF;
         const double* qdd0 = d.qdd0 + w * NF;
         const double D = rp.duration;
-        for (int kind = 0; kind < 2; kind++)
-            for (int i = 0; i < NF; i++) {
-                const double Tq = qd0[i] * D, TTq = qdd0[i] * D * D;
-                const double ka = rp.k_range[i] * x[i];
-                double mn, mx, e2, e3;
-                int mnid, mxid;
-                extremum(kind, q0[i], Tq, TTq, ka, &mn, &mx, &mnid, &mxid, &e2, &e3);
-                const double scale = kind == 0 ? 1.0 : D;
-                const long rmin = off2 + kind * 2 * NF + i, rmax = rmin + NF;
-                const long gmin = rmin, gmax = rmax;
-                Gb[gmin] = mn / scale;
-                Gb[gmax] = mx / scale;
-                const double gmn = extremum_grad(kind, mnid, e2, e3) * rp.k_range[i] / scale;
-                const double gmx = extremum_grad(kind, mxid, e2, e3) * rp.k_range[i] / scale;
+        const int v = tid - ((int)blockDim.x - 2 * NF - 1);
+        if (v < 2 * NF) {
+            const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
+            const int kind = v / NF, i = v % NF;
+            const double Tq = qd0[i] * D, TTq = qdd0[i] * D * D;
+            const double ka = rp.k_range[i] * x[i];
+            double mn, mx, e2, e3;
+            int mnid, mxid;
+            extremum(kind, q0[i], Tq, TTq, ka, &mn, &mx, &mnid, &mxid, &e2, &e3);
+            const double scale = kind == 0 ? 1.0 : D;
+            const long gmin = off2 + kind * 2 * NF + i, gmax = gmin + NF;
+            Gb[gmin] = mn / scale;
+            Gb[gmax] = mx / scale;
+            const double gmn = extremum_grad(kind, mnid, e2, e3) * rp.k_range[i] / scale;
+            const double gmx = extremum_grad(kind, mxid, e2, e3) * rp.k_range[i] / scale;
 #pragma unroll
-                for (int k = 0; k < NF; k++) {
-                    Jb[gmin * NF + k] = (k == i) ? gmn : 0.0;
-                    Jb[gmax * NF + k] = (k == i) ? gmx : 0.0;
+            for (int k = 0; k < NF; k++) {
+                Jb[gmin * NF + k] = (k == i) ? gmn : 0.0;
+                Jb[gmax * NF + k] = (k == i) ? gmx : 0.0;
+            }
+        } else {
+            // cost: wrapped joints summed first (NLPclass.cu:225-233)
+            const double tp = rp.t_plan;
+            double qp[NF];
+            for (int i = 0; i < NF; i++) qp[i] = bz_q(q0[i], qd0[i] * D, qdd0[i] * D * D, rp.k_range[i] * x[i], tp);
+            double fv = 0.0;
+            bool first = true;
+            for (int pass = 1; pass >= 0; pass--)
+                for (int i = 0; i < NF; i++) {
+                    if (rp.wrap_mask[i] != pass) continue;
+                    const double dd = pass ? wrap_to_pi(d.qdes[w * NF + i] - qp[i]) : (d.qdes[w * NF + i] - qp[i]);
+                    const double term = dd * dd;
+                    fv = first ? term : fv + term;
+                    first = false;
                 }
-            }
-        // cost: wrapped joints summed first (NLPclass.cu:225-233)
-        const double tp = rp.t_plan;
-        double qp[NF];
-        for (int i = 0; i < NF; i++) qp[i] = bz_q(q0[i], qd0[i] * D, qdd0[i] * D * D, rp.k_range[i] * x[i], tp);
-        double fv = 0.0;
-        bool first = true;
-        for (int pass = 1; pass >= 0; pass--)
+            *fb = fv * rp.cost_scale;
             for (int i = 0; i < NF; i++) {
-                if (rp.wrap_mask[i] != pass) continue;
-                const double dd = pass ? wrap_to_pi(d.qdes[w * NF + i] - qp[i]) : (d.qdes[w * NF + i] - qp[i]);
-                const double term = dd * dd;
-                fv = first ? term : fv + term;
-                first = false;
+                const double dk = tp * tp * tp * (6 * tp * tp - 15 * tp + 10) * rp.k_range[i];
+                double gv = rp.wrap_mask[i] ? (2 * wrap_to_pi(qp[i] - d.qdes[w * NF + i]) * dk) : (2 * (qp[i] - d.qdes[w * NF + i]) * dk);
+                gradb[i] = gv * rp.cost_scale;
             }
-        *fb = fv * rp.cost_scale;
-        for (int i = 0; i < NF; i++) {
-            const double dk = tp * tp * tp * (6 * tp * tp - 15 * tp + 10) * rp.k_range[i];
-            double gv = rp.wrap_mask[i] ? (2 * wrap_to_pi(qp[i] - d.qdes[w * NF + i]) * dk) : (2 * (qp[i] - d.qdes[w * NF + i]) * dk);
-            gradb[i] = gv * rp.cost_scale;
         }
     }
     __syncthreads();
@@ -771,31 +787,67 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
 #pragma unroll
         for (int j = 0; j < NF; j++) inbox = inbox && fabs(x[j]) <= PC_XBOX;
         if (coll && d.pcready && inbox && d.pcok[jt]) {
+            // the block's records are staged into LDS (the slicing buffer, free now) in chunks of
+            // PC_CH with coalesced loads; each pair keeps its running maximum across chunks
+            constexpr int PPT = (MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS;
+            constexpr int PC_CH = (MAX_J * CAP_LM * 3 + NF * CAP_UM) / 5;
+            double* const S = ubuf;
             const int NP = NJ * O;
             const double* const rec = d.pc + jt * 5 * d.pc_cap;
             const int cap = d.pc_cap;
-            for (int pr = tid; pr < NP; pr += blockDim.x) {
-                const int l = pr / O, o = pr % O;
-                const unsigned po = d.pcoff[jt * NP + pr];
-                const int n = po & 255, q0 = po >> 8;
-                const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
-                double best = -100000000.0, B0 = 0, B1 = 0, B2 = 0;
-                bool isneg = false;
-                for (int q = q0; q < q0 + n; q++) {
-                    const double A0 = rec[q], A1 = rec[cap + q], A2 = rec[2 * cap + q];
-                    const double P = rec[3 * cap + q], N = rec[4 * cap + q];
-                    const double Ac = A0 * c0 + A1 * c1 + A2 * c2;
-                    const double pos = Ac - P;
-                    const double neg = -Ac - N;
-                    if (pos > best) { best = pos; B0 = A0; B1 = A1; B2 = A2; isneg = false; }
-                    if (neg > best) { best = neg; B0 = A0; B1 = A1; B2 = A2; isneg = true; }
-                }
-                const long row = nt + ((long)l * d.T + t) * O + o;
-                Gb[row] = -best;
+            const unsigned* const po = d.pcoff + jt * NP;
+            const unsigned last = po[NP - 1];
+            const int total = (int)(last >> 8) + (int)(last & 255);
+            int q0[PPT], n[PPT];
+            double best[PPT], B[PPT][3];
+            bool isneg[PPT];
 #pragma unroll
-                for (int k = 0; k < NF; k++) {
-                    const double dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
-                    Jb[row * NF + k] = isneg ? dot : -dot;
+            for (int k = 0; k < PPT; k++) {
+                const int pr = tid + k * EVAL_THREADS;
+                const unsigned v = pr < NP ? po[pr] : 0u;
+                q0[k] = (int)(v >> 8);
+                n[k] = (int)(v & 255);
+                best[k] = -100000000.0;
+                B[k][0] = 0; B[k][1] = 0; B[k][2] = 0;
+                isneg[k] = false;
+            }
+            for (int r0 = 0; r0 < total; r0 += PC_CH) {
+                const int m = total - r0 < PC_CH ? total - r0 : PC_CH;
+                __syncthreads();
+                for (int i = tid; i < m; i += blockDim.x) {
+                    const double a0 = rec[r0 + i], a1 = rec[cap + r0 + i], a2 = rec[2 * cap + r0 + i];
+                    const double a3 = rec[3 * cap + r0 + i], a4 = rec[4 * cap + r0 + i];
+                    S[i] = a0; S[PC_CH + i] = a1; S[2 * PC_CH + i] = a2; S[3 * PC_CH + i] = a3; S[4 * PC_CH + i] = a4;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < PPT; k++) {
+                    const int pr = tid + k * EVAL_THREADS;
+                    if (pr >= NP) continue;
+                    const int l = pr / O;
+                    const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
+                    const int lo = (q0[k] > r0 ? q0[k] : r0) - r0, hi = (q0[k] + n[k] < r0 + m ? q0[k] + n[k] : r0 + m) - r0;
+                    for (int q = lo; q < hi; q++) {
+                        const double A0 = S[q], A1 = S[PC_CH + q], A2 = S[2 * PC_CH + q];
+                        const double Ac = A0 * c0 + A1 * c1 + A2 * c2;
+                        const double pos = Ac - S[3 * PC_CH + q];
+                        const double neg = -Ac - S[4 * PC_CH + q];
+                        if (pos > best[k]) { best[k] = pos; B[k][0] = A0; B[k][1] = A1; B[k][2] = A2; isneg[k] = false; }
+                        if (neg > best[k]) { best[k] = neg; B[k][0] = A0; B[k][1] = A1; B[k][2] = A2; isneg[k] = true; }
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < PPT; k++) {
+                const int pr = tid + k * EVAL_THREADS;
+                if (pr >= NP) continue;
+                const int l = pr / O, o = pr % O;
+                const long row = nt + ((long)l * d.T + t) * O + o;
+                Gb[row] = -best[k];
+#pragma unroll
+                for (int kk = 0; kk < NF; kk++) {
+                    const double dot = B[k][0] * dlc[l][kk][0] + B[k][1] * dlc[l][kk][1] + B[k][2] * dlc[l][kk][2];
+                    Jb[row * NF + kk] = isneg[k] ? dot : -dot;
                 }
             }
             coll = false;

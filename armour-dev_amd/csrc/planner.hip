@@ -1036,6 +1036,30 @@ int armour_get_monomial_counts(armour_planner* p, int w, int* link_counts, int* 
     return 0;
 }
 
+int armour_get_plane_cache_stats(armour_planner* p, long long* out, int n) {
+    DeviceScope device_scope(p);
+    if (!p) return fail(ARMOUR_E_ARG, "null planner");
+    if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
+    NlpDev& d = p->d;
+    if (!d.pcache || p->eval_f32 || d.O == 0) return fail(ARMOUR_E_STATE, "plane cache off (ARMOUR_PLANE_CACHE=0, float study or no obstacles)");
+    ensure_plane_cache(p);
+    const size_t blocks = (size_t)p->W * p->T, NP = (size_t)p->NJ * d.O;
+    std::vector<unsigned> off(blocks * NP);
+    std::vector<unsigned char> ok(blocks);
+    HIPCK(hipMemcpyAsync(off.data(), d.pcoff, sizeof(unsigned) * off.size(), hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipMemcpyAsync(ok.data(), d.pcok, blocks, hipMemcpyDeviceToHost, p->stream));
+    HIPCK(hipStreamSynchronize(p->stream));
+    long long kept = 0, nok = 0, mx = 0;
+    for (unsigned v : off) {
+        kept += v & 255;
+        mx = std::max<long long>(mx, v & 255);
+    }
+    for (unsigned char v : ok) nok += v;
+    const long long st[ARMOUR_PC_COUNT] = {kept, (long long)off.size(), nok, (long long)blocks, mx, d.pc_cap};
+    for (int k = 0; k < n && k < ARMOUR_PC_COUNT; k++) out[k] = st[k];
+    return ARMOUR_PC_COUNT;
+}
+
 int armour_get_reach_occupancy(armour_planner* p, long long* used, long long* caps, int n) {
     DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");

@@ -83,3 +83,15 @@ def test_plane_cache_boundary(name):
     rng = np.random.default_rng(11)
     check_eval(P, Q, worlds, rng, n=3)
     check_plan(P, Q, worlds)
+
+
+def test_plane_cache_stats_survey():
+    """kept planes per pair on survey worlds (DESIGN.md section 4 quotes these)"""
+    T, O, W = 100, 20, 64
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    P.reach([A.make_world(2000 + s, O, profile="survey") for s in range(W)])
+    st = P.plane_cache_stats()
+    print("plane cache:", st, "mean kept per pair %.2f" % (st["planes_kept"] / st["pairs"]))
+    assert st["pairs"] == W * T * 7 * O
+    assert st["blocks_cached"] == st["blocks"]
+    assert 1 <= st["max_per_pair"] <= 36
