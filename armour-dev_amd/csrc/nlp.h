@@ -98,7 +98,8 @@ struct NlpDev {
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in
     // the box |x_i| <= PC_XBOX, in the reference's scan order: (world, t) region of pc_cap records
     // [5][pc_cap] (A0 A1 A2, P = d + delta, N = -d + delta), pcoff [W][T][NJ * O] = (first record << 8)
-    // | count, pcok [W][T] = 1 when the region held every survivor (else the block scans in full).
+    // | count, pcok [W][T] = 1 when the region held every survivor (always: pc_cap has room for all
+    // 36 planes of every pair; reads touch only the records kept, ~5 per pair).
     int pcache;             // cache enabled (ARMOUR_PLANE_CACHE=0 disables it)
     int pcready;            // built for the current reach sets and obstacles
     int pc_cap;             // records per (world, t)
@@ -107,7 +108,7 @@ struct NlpDev {
     unsigned char* pcok;
 };
 constexpr int NSPEC = 16;
-constexpr int PC_AVG = 12;             // cache records per pair reserved (mean use ~5)
+constexpr int PC_K = COMB;             // cache records per pair reserved: all 36 planes
 constexpr double PC_XBOX = 1.0 + 1e-6; // certified box of x (the solver keeps |x_i| <= 1)
 constexpr double PC_RADF = 1.0001;     // >= PC_XBOX^21, the largest monomial degree sum (7 x 3)
 constexpr double PC_MARGIN = 1e-9;     // >> the rounding of the bound and of A . c (~1e-15)

@@ -571,8 +571,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
 // copies the current slot's, the final iterate's, out).
 // ARMTD selects the comparison planner's extrema and cost at compile time: a call into them from
 // the ARMOUR instantiation would cost it registers and a stack frame (occupancy 4 -> 3 waves/SIMD)
-template <typename R, bool ARMTD>
+// CACHED (fp64 only): the collision rows from the certified plane cache, for points in its box
+// (every solver point; armour_eval_constraints checks x on the host); otherwise the full scan
+template <typename R, bool ARMTD, bool CACHED>
 __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
+    static_assert(!CACHED || std::is_same<R, double>::value, "the plane cache is fp64");
     // mode 3: speculative trial k of list entry i (blockIdx.y = i * K + k) into its own slot
     if (mode == 1 && d.lcount && blockIdx.y >= *d.lcount) return;
     const int t = blockIdx.x, w = mode == 3 ? d.wl[blockIdx.y / d.K] : world_of(d, blockIdx.y);
@@ -625,8 +628,10 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     }
     if (tid < NJ) lcnt[tid] = d.ro.link_cnt[jt * NJ + tid];
     if (tid >= 32 && tid < 32 + NF) tcnt[tid - 32] = d.nt ? d.ro.tq_cnt[jt * NF + tid - 32] : 0;  // ARMTD: no torque PZs
-    for (int i = tid; i < NJ * 18; i += blockDim.x) lgen[i / 18][i % 18] = d.ro.link_gens[jt * NJ * 18 + i];
-    for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
+    if constexpr (!CACHED) {
+        for (int i = tid; i < NJ * 18; i += blockDim.x) lgen[i / 18][i % 18] = d.ro.link_gens[jt * NJ * 18 + i];
+        for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
+    }
     __syncthreads();
     if (!(d.diag & 1)) {
         // only the valid monomials, enumerated compactly (one load round per thread): u < L are
@@ -780,13 +785,19 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     // completes them.
     const long nt = d.nt;
     bool coll = !(d.diag & 2);
-    if constexpr (std::is_same<R, double>::value) {
-        // the certified plane cache (plane_cache_kernel) when it holds this block's planes and x lies in
-        // its box: the scan over the surviving planes, same order, same arithmetic
+    if constexpr (CACHED) {
+        // the certified plane cache (plane_cache_kernel): the scan over the kept planes, same order,
+        // same arithmetic. A point outside the cache's box cannot come from the solver (its box
+        // slacks keep |x_i| <= 1 up to rounding); should one arrive, its rows are NaN (the line
+        // search rejects the trial) and the miss is counted (armour_get_plane_cache_stats).
         bool inbox = true;
 #pragma unroll
         for (int j = 0; j < NF; j++) inbox = inbox && fabs(x[j]) <= PC_XBOX;
-        if (coll && d.pcready && inbox && d.pcok[jt]) {
+        if (coll && !inbox) {
+            for (int pr = tid; pr < NJ * O; pr += blockDim.x)
+                Gb[nt + ((long)(pr / O) * d.T + t) * O + pr % O] = __builtin_nan("");
+            if (tid == 0) atomicAdd(d.cnt + 7, 1u);
+        } else if (coll) {
             // the block's records are staged into LDS (the slicing buffer, free now) in chunks of
             // PC_CH with coalesced loads; each pair keeps its running maximum across chunks
             constexpr int PPT = (MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS;
@@ -853,6 +864,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
             coll = false;
         }
     }
+    if constexpr (!CACHED) {
     for (int u = tid; u < (coll ? NJ * LL_PLANES + O * OO_PLANES : 0); u += blockDim.x) {
         if (u < NJ * LL_PLANES) {
             const int l = u / LL_PLANES, p = u % LL_PLANES;
@@ -976,15 +988,18 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
             Jb[row * NF + k] = isneg ? dot : -dot;
         }
     }
+    }
 }
 
 // the product evaluation is fp64; eval_kernel_t<float> serves only the fp32 tolerance study
 // (ARMOUR_EVAL_F32, tools/fp32_study.py): reach sets stay fp64, the slicing and collision
 // arithmetic runs in float
-template __global__ void eval_kernel_t<double, false>(NlpDev, int);
-template __global__ void eval_kernel_t<float, false>(NlpDev, int);
-template __global__ void eval_kernel_t<double, true>(NlpDev, int);
-template __global__ void eval_kernel_t<float, true>(NlpDev, int);
+template __global__ void eval_kernel_t<double, false, false>(NlpDev, int);
+template __global__ void eval_kernel_t<float, false, false>(NlpDev, int);
+template __global__ void eval_kernel_t<double, true, false>(NlpDev, int);
+template __global__ void eval_kernel_t<float, true, false>(NlpDev, int);
+template __global__ void eval_kernel_t<double, false, true>(NlpDev, int);
+template __global__ void eval_kernel_t<double, true, true>(NlpDev, int);
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM

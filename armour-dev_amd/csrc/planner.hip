@@ -373,7 +373,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // certified plane cache: PC_AVG records per (link, obstacle) pair of every (world, t)
     d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
     d.pcready = 0;
-    d.pc_cap = PC_AVG * NJ * Om;
+    d.pc_cap = PC_K * NJ * Om;
     if (d.pcache && ((rc = p->alloc(&d.pc, jobs * 5 * (size_t)d.pc_cap)) || (rc = p->alloc(&d.pcoff, jobs * NJ * (size_t)Om)) ||
                      (rc = p->alloc(&d.pcok, jobs))))
         return rc;
@@ -575,9 +575,13 @@ static int nside_count(const armour_planner* p) {
 
 // g and J of every world of the batch (eval_kernel_t): fp64, or float for the tolerance study
 // (the ARMTD planner's extrema and cost in their own instantiation)
-static void launch_eval(armour_planner* p, dim3 grid, const NlpDev& d, int mode) {
-    auto k = p->eval_f32 ? (d.armtd ? eval_kernel_t<float, true> : eval_kernel_t<float, false>)
-                         : (d.armtd ? eval_kernel_t<double, true> : eval_kernel_t<double, false>);
+// and the collision rows from the certified plane cache when it is built (points in its box: every
+// solver point; `cached` = false for a caller's x outside it)
+static void launch_eval(armour_planner* p, dim3 grid, const NlpDev& d, int mode, bool cached = true) {
+    const bool c = cached && d.pcready && d.O > 0;
+    auto k = p->eval_f32 ? (d.armtd ? eval_kernel_t<float, true, false> : eval_kernel_t<float, false, false>)
+                         : c ? (d.armtd ? eval_kernel_t<double, true, true> : eval_kernel_t<double, false, true>)
+                             : (d.armtd ? eval_kernel_t<double, true, false> : eval_kernel_t<double, false, false>);
     hipLaunchKernelGGL(k, grid, dim3(EVAL_THREADS), 0, p->stream, d, mode);
 }
 
@@ -940,7 +944,9 @@ int armour_eval_constraints(armour_planner* p, int w, const double* x, double* g
     }
     HIPCK(hipMemcpyAsync(d.ws, ws.data(), sizeof(WorldState) * p->W, hipMemcpyHostToDevice, p->stream));
     ensure_plane_cache(p);
-    launch_eval(p, dim3(p->T, p->W), d, 0);
+    bool inbox = true;
+    for (int j = 0; j < NF; j++) inbox = inbox && std::fabs(x[j]) <= PC_XBOX;
+    launch_eval(p, dim3(p->T, p->W), d, 0, inbox);
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(g, d.g + gidx(d, 0, w, 0), sizeof(double) * d.m, hipMemcpyDeviceToHost, p->stream));
     if (jac) HIPCK(hipMemcpyAsync(jac, d.J + gidx(d, 0, w, 0) * NF, sizeof(double) * d.m * NF, hipMemcpyDeviceToHost, p->stream));
@@ -1055,7 +1061,9 @@ int armour_get_plane_cache_stats(armour_planner* p, long long* out, int n) {
         mx = std::max<long long>(mx, v & 255);
     }
     for (unsigned char v : ok) nok += v;
-    const long long st[ARMOUR_PC_COUNT] = {kept, (long long)off.size(), nok, (long long)blocks, mx, d.pc_cap};
+    unsigned miss = 0;
+    HIPCK(hipMemcpy(&miss, d.cnt + 7, sizeof(unsigned), hipMemcpyDeviceToHost));
+    const long long st[ARMOUR_PC_COUNT] = {kept, (long long)off.size(), nok, (long long)blocks, mx, d.pc_cap, miss};
     for (int k = 0; k < n && k < ARMOUR_PC_COUNT; k++) out[k] = st[k];
     return ARMOUR_PC_COUNT;
 }
