@@ -30,6 +30,8 @@ struct WorldState {
     double x[NF], xt[NF], dx[NF];
     double H[NF * NF];
     double mu, alpha, ap, ad, theta0, phi0, Dphi, theta_max, theta_min, kkt;
+    double sw_dphi, sw_theta;          // pow(-Dphi, 2.3) (Dphi < 0) and pow(theta0, 1.1) of this
+                                       // iteration: the switching condition's powers, once per iteration
     double wa_old_a[NF], wa_old_b[NF];   // sum (z_lo - z_hi) a  and  sum (dz_lo - dz_hi) a at x
     double filt_theta[MAX_FILTER], filt_phi[MAX_FILTER];
     int nfilt;
@@ -61,9 +63,16 @@ struct NlpDev {
     ReachOut ro;
     // row bounds [W][R]
     double *L, *U;
-    // evaluation slots: g [2][W][m], J [2][W][m][NF], f [2][W], grad [2][W][NF]
+    // evaluation slots: g [2][W][m], J [2][W][m][NF], f [2][W], grad [2][W][NF]. The collision
+    // rows' Jacobian is held compactly: row (l, t, o) is J = n . dc/dx with n the winning plane's
+    // signed normal, jn [2][W][T * NJ * O][3], and dc/dx the sliced link centre's derivatives,
+    // jd [2][W][T][NJ][NF][3] (shared by the row's O obstacles); J keeps the other rows (and, after a
+    // start-point / caller evaluation, mode 0, the collision rows dense too). row_va expands them.
     double* g;
     double* J;
+    double* jn;
+    double* jd;
+    long njn, njd;          // per-slot sizes of jn, jd (W * T * NJ * Omax * 3, W * T * NJ * NF * 3)
     double* f;
     double* grad;
     double* link_c;         // [3][lcs]: [slot][W][T][NJ][3] sliced link centres of each eval slot's
@@ -92,7 +101,7 @@ struct NlpDev {
     // searching worlds evaluated at once into their own slots, [list entry i][trial k] (see
     // ipm_world_Cs); the trial that ends the search is copied into the world's trial slot.
     int K;
-    double *gs, *Js, *fs, *grads, *lcs_s, *partial_s;
+    double *gs, *Js, *fs, *grads, *lcs_s, *partial_s, *jns, *jds;
     // Certified plane cache (plane_cache_kernel). The 36 planes of a buffered
     // obstacle and their offsets d, delta do not depend on x; only A . c(x) does. For every
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in

@@ -58,11 +58,28 @@ __device__ inline void block_reduce_n(double (&v)[N], const int (&kinds)[N], dou
     }
 }
 
+// row bounds: a collision row's are the constants bounds_kernel stores (-1e19, 0), not re-read
+__device__ inline void row_bounds(const NlpDev& d, long i, int r, double& L, double& U) {
+    const bool col = r >= d.nt && r < d.nt + d.T * d.NJ * d.O;
+    L = col ? -1e19 : d.L[i];
+    U = col ? 0.0 : d.U[i];
+}
 __device__ inline bool has_lo(const NlpDev& d, double L) { return L > -d.opt.inf_bound; }
 __device__ inline bool has_hi(const NlpDev& d, double U) { return U < d.opt.inf_bound; }
 
-// value and gradient of row r of world w from eval slot `slot` at point x
+// value and gradient of row r of world w from eval slot `slot` at point x; a collision row's
+// gradient is n . dc/dx from the compact form (bitwise the value eval_kernel forms densely)
 __device__ inline double row_va(const NlpDev& d, int slot, int w, int r, const double* x, double* a) {
+    const int nc = d.T * d.NJ * d.O;
+    if (r >= d.nt && r < d.nt + nc) {
+        const int q = r - d.nt, lt = q / d.O, l = lt / d.T, t = lt % d.T;
+        const double* n = d.jn + slot * d.njn + ((long)w * nc + q) * 3;
+        const double* D = d.jd + slot * d.njd + (((long)w * d.T + t) * d.NJ + l) * NF * 3;
+        const double n0 = n[0], n1 = n[1], n2 = n[2];
+#pragma unroll
+        for (int j = 0; j < NF; j++) a[j] = n0 * D[3 * j] + n1 * D[3 * j + 1] + n2 * D[3 * j + 2];
+        return d.g[gidx(d, slot, w, r)];
+    }
     if (r < d.m) {
         const long gi = gidx(d, slot, w, r);
         const double* J = d.J + gi * NF;
@@ -588,6 +605,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
                                   : d.link_c + slot * d.lcs + (long)w * d.T * d.NJ * 3;
     double* const fb = mode == 3 ? d.fs + blockIdx.y : d.f + slot * d.W + w;
     double* const gradb = mode == 3 ? d.grads + (long)blockIdx.y * NF : d.grad + ((long)slot * d.W + w) * NF;
+    // compact collision Jacobian (NlpDev::jn / jd); mode 0 also writes those rows densely into Jb
+    const long ncol = (long)d.T * d.NJ * d.O;
+    double* const Jnb = mode == 3 ? d.jns + (long)blockIdx.y * ncol * 3 : d.jn + slot * d.njn + (long)w * ncol * 3;
+    double* const Jdb = mode == 3 ? d.jds + (long)blockIdx.y * d.T * d.NJ * NF * 3
+                                  : d.jd + slot * d.njd + (long)w * d.T * d.NJ * NF * 3;
     const RobotParams& rp = *d.rp;
     const int tid = threadIdx.x;
     const long jt = (long)w * d.T + t;
@@ -698,6 +720,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
             Lcb[((long)t * NJ + l) * 3 + e] = cc;
         } else {
             dlc[l][k - 1][e] = c;
+            Jdb[(((long)t * NJ + l) * NF + k - 1) * 3 + e] = c;
         }
       } else {
         // torque rows (NLPclass.cu:304-309, 376-380)
@@ -855,10 +878,17 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
                 const int l = pr / O, o = pr % O;
                 const long row = nt + ((long)l * d.T + t) * O + o;
                 Gb[row] = -best[k];
+                // J = isneg ? B . dc : -(B . dc) = n . dc with n = isneg ? B : -B (negation is exact)
+                double* const jn = Jnb + (row - nt) * 3;
+                jn[0] = isneg[k] ? B[k][0] : -B[k][0];
+                jn[1] = isneg[k] ? B[k][1] : -B[k][1];
+                jn[2] = isneg[k] ? B[k][2] : -B[k][2];
+                if (mode == 0) {
 #pragma unroll
-                for (int kk = 0; kk < NF; kk++) {
-                    const double dot = B[k][0] * dlc[l][kk][0] + B[k][1] * dlc[l][kk][1] + B[k][2] * dlc[l][kk][2];
-                    Jb[row * NF + kk] = isneg[k] ? dot : -dot;
+                    for (int kk = 0; kk < NF; kk++) {
+                        const double dot = B[k][0] * dlc[l][kk][0] + B[k][1] * dlc[l][kk][1] + B[k][2] * dlc[l][kk][2];
+                        Jb[row * NF + kk] = isneg[k] ? dot : -dot;
+                    }
                 }
             }
             coll = false;
@@ -982,10 +1012,16 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
         if (mwin >= 0) plane_normal(obs[o] + 3 * (mwin / 6 + 1), lgen[l] + 3 * (mwin % 6), B0, B1, B2);
         const long row = nt + ((long)l * d.T + t) * O + o;
         Gb[row] = -best;
+        double* const jn = Jnb + (row - nt) * 3;
+        jn[0] = isneg ? B0 : -B0;
+        jn[1] = isneg ? B1 : -B1;
+        jn[2] = isneg ? B2 : -B2;
+        if (mode == 0) {
 #pragma unroll
-        for (int k = 0; k < NF; k++) {
-            const R dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
-            Jb[row * NF + k] = isneg ? dot : -dot;
+            for (int k = 0; k < NF; k++) {
+                const R dot = B0 * dlc[l][k][0] + B1 * dlc[l][k][1] + B2 * dlc[l][k][2];
+                Jb[row * NF + k] = isneg ? dot : -dot;
+            }
         }
     }
     }
@@ -1039,7 +1075,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
         double a[NF];
         const double v = row_va(d, S.cur, w, (int)r, S.x, a);
         const long i = (long)w * d.R + r;
-        const double L = d.L[i], U = d.U[i];
+        double L, U;
+        row_bounds(d, i, (int)r, L, U);
         const bool hl = has_lo(d, L), hh = has_hi(d, U);
         double p = 0;
         if (hl && hh) p = fmin(d.opt.bound_push * fmax(1.0, fabs(L)), d.opt.bound_push * (U - L));
@@ -1075,7 +1112,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
         double a[NF];
         const double v = row_va(d, S.cur, w, (int)r, S.x, a);
         const long i = (long)w * d.R + r;
-        const double L = d.L[i], U = d.U[i];
+        double L, U;
+        row_bounds(d, i, (int)r, L, U);
         double wr = 0, sig = 0, c1 = 0, c2 = 0;
         if (has_lo(d, L)) {
             const double s = d.slo[i], z = d.zlo[i];
@@ -1258,7 +1296,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
 #pragma unroll
         for (int j = 0; j < NF; j++) adx += a[j] * S.dx[j];
         const long i = (long)w * d.R + r;
-        const double L = d.L[i], U = d.U[i];
+        double L, U;
+        row_bounds(d, i, (int)r, L, U);
         double za = 0, zb = 0;
         if (has_lo(d, L)) {
             const double s = d.slo[i], z = d.zlo[i], sg = z / s;
@@ -1315,6 +1354,8 @@ __global__ void ipm_world_B(NlpDev d) {
     if (S.theta_max < 0) S.theta_max = 1e4 * fmax(1.0, S.theta0);
     S.phi0 = f - S.mu * P[4];
     S.Dphi = gdx - S.mu * P[3];
+    S.sw_dphi = S.Dphi < 0 ? pow(-S.Dphi, 2.3) : 0.0;
+    S.sw_theta = pow(S.theta0, 1.1);
     for (int j = 0; j < NF; j++) { S.wa_old_a[j] = P[5 + j]; S.wa_old_b[j] = P[12 + j]; }
     S.alpha = S.ap;
     for (int j = 0; j < NF; j++) S.xt[j] = S.x[j] + S.alpha * S.dx[j];
@@ -1337,7 +1378,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
         double a[NF];
         const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
         const long i = (long)w * d.R + r;
-        const double L = d.L[i], U = d.U[i];
+        double L, U;
+        row_bounds(d, i, (int)r, L, U);
         if (has_lo(d, L)) { const double st = d.slo[i] + S.alpha * d.dslo[i]; logt += log(st); rpt += fabs((v - L) - st); }
         if (has_hi(d, U)) { const double st = d.shi[i] + S.alpha * d.dshi[i]; logt += log(st); rpt += fabs((U - v) - st); }
     }
@@ -1369,7 +1411,7 @@ __device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt,
         if (!(thetat < S.filt_theta[q] || phit < S.filt_phi[q])) ok = false;
     bool ftype = false;
     if (ok) {
-        const bool switching = S.Dphi < 0 && S.alpha * pow(-S.Dphi, 2.3) > pow(S.theta0, 1.1);
+        const bool switching = S.Dphi < 0 && S.alpha * S.sw_dphi > S.sw_theta;
         if (switching && S.theta0 <= S.theta_min) {
             ok = phit <= S.phi0 + d.opt.eta * S.alpha * S.Dphi;
             ftype = ok;
@@ -1444,7 +1486,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
         const double v = r < d.m ? G[r] : xt[r - d.m];
         const long ii = (long)w * d.R + r;
-        const double L = d.L[ii], U = d.U[ii];
+        double L, U;
+        row_bounds(d, ii, (int)r, L, U);
         if (has_lo(d, L)) { const double st = d.slo[ii] + alpha * d.dslo[ii]; logt += log(st); rpt += fabs((v - L) - st); }
         if (has_hi(d, U)) { const double st = d.shi[ii] + alpha * d.dshi[ii]; logt += log(st); rpt += fabs((U - v) - st); }
     }
@@ -1456,21 +1499,27 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
 
 // the trials of a speculative round tested in order, exactly as the sequential rounds would
 // (ipm_world_C): the first acceptable one ends the search, or the last (forced) one
+// list entry blockIdx.x (one wave): every trial's two partial sums at once (lane 2 k + q, block
+// partials summed in order as world_partials_at), then the acceptance tests in trial order on lane 0
 __global__ void ipm_world_Cs(NlpDev d) {
-    const int w = d.wl[blockIdx.x];
+    const int i = blockIdx.x, w = d.wl[i];
     WorldState& S = d.ws[w];
+    const int lane = threadIdx.x & 63;
+    double s = 0.0;
+    if (lane < 2 * d.K) {
+        const double* in = d.partial_s + ((long)i * d.K + (lane >> 1)) * d.nblk * KA + (lane & 1);
+        for (int b = 0; b < d.nblk; b++) s = s + in[(long)b * KA];
+    }
+    const uint64_t u = __builtin_bit_cast(uint64_t, s);
     int chosen = -1;
     for (int k = 0; k < d.K; k++) {
-        int go = 0;
-        if (threadIdx.x == 0) go = S.status == 0 && S.searching;
-        if (!__shfl(go, 0)) break;
-        double P[2];
-        const double init[2] = {0.0, 0.0};
-        const int op[2] = {0, 0};
-        const long sidx = (long)blockIdx.x * d.K + k;
-        world_partials_at(d.partial_s + sidx * d.nblk * KA, d.nblk, init, op, P);
-        if (threadIdx.x == 0) {
-            accept_trial(d, S, P[0], P[1], d.fs[sidx]);
+        const uint32_t lo0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 2 * k);
+        const uint32_t hi0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 2 * k);
+        const uint32_t lo1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 2 * k + 1);
+        const uint32_t hi1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 2 * k + 1);
+        if (threadIdx.x == 0 && chosen == k - 1 && S.status == 0 && S.searching) {
+            accept_trial(d, S, __builtin_bit_cast(double, ((uint64_t)hi0 << 32) | lo0),
+                         __builtin_bit_cast(double, ((uint64_t)hi1 << 32) | lo1), d.fs[(long)i * d.K + k]);
             chosen = k;
         }
     }
@@ -1484,18 +1533,33 @@ __global__ void ipm_copy_spec(NlpDev d) {
     if (S.spec_k < 0) return;
     const long sidx = (long)blockIdx.y * d.K + S.spec_k;
     const int slot = 1 - S.cur;
-    const long nlc = (long)d.T * d.NJ * 3, nj = (long)d.m * NF;
-    const long n = d.m + nj + nlc;
+    const long nlc = (long)d.T * d.NJ * 3, nc = (long)d.T * d.NJ * d.O;
+    const long nj0 = (long)d.nt * NF, nj1 = (d.m - d.nt - nc) * NF;  // dense J rows: before / after the collision rows
+    const long njn = nc * 3, njd = (long)d.T * d.NJ * NF * 3;
+    const long n = d.m + nj0 + nj1 + njn + njd + nlc;
     double* g = d.g + gidx(d, slot, w, 0);
     double* J = d.J + gidx(d, slot, w, 0) * NF;
+    double* jn = d.jn + slot * d.njn + (long)w * njn;
+    double* jd = d.jd + slot * d.njd + (long)w * njd;
     double* lc = d.link_c + slot * d.lcs + (long)w * nlc;
     const double* gs = d.gs + sidx * d.m;
-    const double* Js = d.Js + sidx * nj;
+    const double* Js = d.Js + sidx * d.m * NF;
+    const double* jns = d.jns + sidx * njn;
+    const double* jds = d.jds + sidx * njd;
     const double* ls = d.lcs_s + sidx * nlc;
     for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
-        if (q < d.m) g[q] = gs[q];
-        else if (q < d.m + nj) J[q - d.m] = Js[q - d.m];
-        else lc[q - d.m - nj] = ls[q - d.m - nj];
+        long u = q;
+        if (u < d.m) { g[u] = gs[u]; continue; }
+        u -= d.m;
+        if (u < nj0) { J[u] = Js[u]; continue; }
+        u -= nj0;
+        if (u < nj1) { J[(d.nt + nc) * NF + u] = Js[(d.nt + nc) * NF + u]; continue; }
+        u -= nj1;
+        if (u < njn) { jn[u] = jns[u]; continue; }
+        u -= njn;
+        if (u < njd) { jd[u] = jds[u]; continue; }
+        u -= njd;
+        lc[u] = ls[u];
     }
     if (blockIdx.x == 0 && threadIdx.x < NF) {
         d.grad[((long)slot * d.W + w) * NF + threadIdx.x] = d.grads[sidx * NF + threadIdx.x];
@@ -1518,7 +1582,8 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
         double a[NF];
         row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
         const long i = (long)w * d.R + r;
-        const double L = d.L[i], U = d.U[i];
+        double L, U;
+        row_bounds(d, i, (int)r, L, U);
         double wv = 0;
         if (has_lo(d, L)) {
             const double zn = d.zlo[i] + ad * d.dzlo[i];

@@ -347,6 +347,9 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         (rc = p->alloc(&d.J, 2 * Wm * mmax * NF)) || (rc = p->alloc(&d.f, 2 * (size_t)Wm)) ||
         (rc = p->alloc(&d.grad, 2 * (size_t)Wm * NF)) || (rc = p->alloc(&d.link_c, 3 * jobs * NJ * 3)))
         return rc;
+    d.njn = (long)(jobs * NJ * Om * 3);
+    d.njd = (long)(jobs * NJ * NF * 3);
+    if ((rc = p->alloc(&d.jn, 2 * (size_t)d.njn)) || (rc = p->alloc(&d.jd, 2 * (size_t)d.njd))) return rc;
     double** rowbufs[] = {&d.slo, &d.shi, &d.zlo, &d.zhi, &d.dslo, &d.dshi, &d.dzlo, &d.dzhi, &d.rplo, &d.rphi};
     for (double** b : rowbufs)
         if ((rc = p->alloc(b, Wm * Rmax))) return rc;
@@ -367,6 +370,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         const size_t ns = (size_t)std::min(Wm, NSPEC) * d.K;
         if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.Js, ns * mmax * NF)) || (rc = p->alloc(&d.fs, ns)) ||
             (rc = p->alloc(&d.grads, ns * NF)) || (rc = p->alloc(&d.lcs_s, ns * T * NJ * 3)) ||
+            (rc = p->alloc(&d.jns, ns * T * NJ * Om * 3)) || (rc = p->alloc(&d.jds, ns * T * NJ * NF * 3)) ||
             (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
             return rc;
     }

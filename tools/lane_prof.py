@@ -10,7 +10,7 @@ T, O, W = 100, 20, int(os.environ.get('LP_W', 256))
 names = ['JRS', 'MAKE1D', 'MAKEROT', 'MAKEBOX', 'CONST', 'ZERO', 'VIEW', 'TRANSPOSE', 'MUL', 'ADD', 'STACK3', 'ADD1D',
          'EMIT_LINK', 'EMIT_TORQUE', 'TORQUE_RADIUS', 'CROSS_C', 'CROSS_PP']
 P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
-ws = [A.make_world(100 + s, O) for s in range(W)]
+ws = [A.make_world(100 + s, O, profile=os.environ.get('LP_PROFILE', 'survey')) for s in range(W)]
 tm = P.reach(ws)
 print('reach', tm)
 import ctypes
