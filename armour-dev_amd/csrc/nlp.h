@@ -97,11 +97,12 @@ struct NlpDev {
     // of the list it appends to into lcount_out
     const unsigned* lcount;
     unsigned* lcount_out;
-    // Speculative line-search round: the remaining K = max_ls - 1 trial points of up to NSPEC
-    // searching worlds evaluated at once into their own slots, [list entry i][trial k] (see
-    // ipm_world_Cs); the trial that ends the search is copied into the world's trial slot.
+    // Speculative line-search round: the values (g, f) of the remaining K = max_ls - 1 trial points
+    // of every world still searching after round 0, [list entry i][trial k] (eval_trials_kernel,
+    // ipm_world_Cs); the trial that ends the search is then evaluated in full into the world's trial
+    // slot (eval_kernel_t mode 5).
     int K;
-    double *gs, *Js, *fs, *grads, *lcs_s, *partial_s, *jns, *jds;
+    double *gs, *fs, *partial_s;
     // Certified plane cache (plane_cache_kernel). The 36 planes of a buffered
     // obstacle and their offsets d, delta do not depend on x; only A . c(x) does. For every
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in
@@ -116,7 +117,7 @@ struct NlpDev {
     unsigned* pcoff;
     unsigned char* pcok;
 };
-constexpr int NSPEC = 16;
+constexpr int EV_MAXK = 9;   // speculative trials per world (max_ls - 1)
 constexpr int PC_K = COMB;             // cache records per pair reserved: all 36 planes
 constexpr double PC_XBOX = 1.0 + 1e-6; // certified box of x (the solver keeps |x_i| <= 1)
 constexpr double PC_RADF = 1.0001;     // >= PC_XBOX^21, the largest monomial degree sum (7 x 3)

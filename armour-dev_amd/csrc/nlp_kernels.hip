@@ -593,23 +593,23 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
 template <typename R, bool ARMTD, bool CACHED>
 __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
     static_assert(!CACHED || std::is_same<R, double>::value, "the plane cache is fp64");
-    // mode 3: speculative trial k of list entry i (blockIdx.y = i * K + k) into its own slot
+    // mode 5: the trial point the speculative round chose (ipm_world_Cs: spec_k >= 0), in full,
+    // into the world's trial slot (list entries, blockIdx.y -> wl)
     if (mode == 1 && d.lcount && blockIdx.y >= *d.lcount) return;
-    const int t = blockIdx.x, w = mode == 3 ? d.wl[blockIdx.y / d.K] : world_of(d, blockIdx.y);
+    const int t = blockIdx.x, w = world_of(d, blockIdx.y);
     WorldState& S = d.ws[w];
-    if (mode >= 1 && !(S.status == 0 && S.searching)) return;
+    if (mode == 1 && !(S.status == 0 && S.searching)) return;
+    if (mode == 5 && !(S.status == 0 && S.spec_k >= 0)) return;
     const int slot = mode == 0 ? 0 : 1 - S.cur;
-    double* const Gb = mode == 3 ? d.gs + (long)blockIdx.y * d.m : d.g + gidx(d, slot, w, 0);
-    double* const Jb = mode == 3 ? d.Js + (long)blockIdx.y * d.m * NF : d.J + gidx(d, slot, w, 0) * NF;
-    double* const Lcb = mode == 3 ? d.lcs_s + (long)blockIdx.y * d.T * d.NJ * 3
-                                  : d.link_c + slot * d.lcs + (long)w * d.T * d.NJ * 3;
-    double* const fb = mode == 3 ? d.fs + blockIdx.y : d.f + slot * d.W + w;
-    double* const gradb = mode == 3 ? d.grads + (long)blockIdx.y * NF : d.grad + ((long)slot * d.W + w) * NF;
+    double* const Gb = d.g + gidx(d, slot, w, 0);
+    double* const Jb = d.J + gidx(d, slot, w, 0) * NF;
+    double* const Lcb = d.link_c + slot * d.lcs + (long)w * d.T * d.NJ * 3;
+    double* const fb = d.f + slot * d.W + w;
+    double* const gradb = d.grad + ((long)slot * d.W + w) * NF;
     // compact collision Jacobian (NlpDev::jn / jd); mode 0 also writes those rows densely into Jb
     const long ncol = (long)d.T * d.NJ * d.O;
-    double* const Jnb = mode == 3 ? d.jns + (long)blockIdx.y * ncol * 3 : d.jn + slot * d.njn + (long)w * ncol * 3;
-    double* const Jdb = mode == 3 ? d.jds + (long)blockIdx.y * d.T * d.NJ * NF * 3
-                                  : d.jd + slot * d.njd + (long)w * d.T * d.NJ * NF * 3;
+    double* const Jnb = d.jn + slot * d.njn + (long)w * ncol * 3;
+    double* const Jdb = d.jd + slot * d.njd + (long)w * d.T * d.NJ * NF * 3;
     const RobotParams& rp = *d.rp;
     const int tid = threadIdx.x;
     const long jt = (long)w * d.T + t;
@@ -637,12 +637,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     __shared__ int lcnt[MAX_J], tcnt[NF];
     __shared__ R ptab[NF][8];
     if (tid < NF) {
-        double xd = mode == 1 ? S.xt[tid] : S.x[tid];
-        if (mode == 3) {  // alpha halved k times and x + alpha dx: ipm_world_C's arithmetic
-            double a = S.alpha;
-            for (int k = 0; k < (int)(blockIdx.y % d.K); k++) a *= 0.5;
-            xd = S.x[tid] + a * S.dx[tid];
-        }
+        const double xd = mode == 0 ? S.x[tid] : S.xt[tid];
         x[tid] = xd;
         const R xj = (R)xd;
         ptab[tid][0] = (R)1.0; ptab[tid][1] = xj; ptab[tid][2] = xj * xj; ptab[tid][3] = xj * xj * xj;
@@ -1036,6 +1031,213 @@ template __global__ void eval_kernel_t<double, true, false>(NlpDev, int);
 template __global__ void eval_kernel_t<float, true, false>(NlpDev, int);
 template __global__ void eval_kernel_t<double, false, true>(NlpDev, int);
 template __global__ void eval_kernel_t<double, true, true>(NlpDev, int);
+
+// ------------------------------------------------------------------------------------------
+// Speculative line-search round, values only. Block (t, list entry i) evaluates the K = max_ls - 1
+// remaining trial points of world wl[i] (alpha halved k times from the round's alpha: the points
+// ipm_world_C's sequential rounds would visit) — the constraint values and the cost, all the
+// acceptance test reads (ipm_rows_Cs / ipm_world_Cs); the Jacobian is formed only for the trial
+// chosen, by a full evaluation (eval_kernel_t mode 5). The monomials and the certified-plane
+// records are staged once for all K points; every value is formed with eval_kernel_t's arithmetic.
+__global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
+    const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
+    const WorldState& S = d.ws[w];
+    if (!(S.status == 0 && S.searching)) return;
+    const RobotParams& rp = *d.rp;
+    const int tid = threadIdx.x, K = d.K;
+    const long jt = (long)w * d.T + t;
+    const int NJ = d.NJ, O = d.O, NP = NJ * O;
+    const long nt = d.nt;
+    __shared__ double xk[EV_MAXK][NF];
+    __shared__ double ptab[EV_MAXK][NF][4];  // x_j^g of trial k (the value slices' factors)
+    __shared__ double lck[EV_MAXK][MAX_J][3];
+    __shared__ uint16_t lh[MAX_J][CAP_LM];
+    __shared__ uint16_t th[NF][CAP_UM];
+    __shared__ double ubuf[MAX_J * CAP_LM * 3 + NF * CAP_UM];
+    __shared__ int lcnt[MAX_J], tcnt[NF];
+    auto lco = reinterpret_cast<double (*)[CAP_LM][3]>(ubuf);
+    auto tco = reinterpret_cast<double (*)[CAP_UM]>(ubuf + MAX_J * CAP_LM * 3);
+    if (tid < K * NF) {
+        const int kk = tid / NF, j = tid % NF;
+        double a = S.alpha;
+        for (int q = 0; q < kk; q++) a *= 0.5;
+        const double xj = S.x[j] + a * S.dx[j];
+        xk[kk][j] = xj;
+        ptab[kk][j][0] = 1.0; ptab[kk][j][1] = xj; ptab[kk][j][2] = xj * xj; ptab[kk][j][3] = xj * xj * xj;
+    }
+    if (tid >= 64 && tid < 64 + NJ) lcnt[tid - 64] = d.ro.link_cnt[jt * NJ + tid - 64];
+    if (tid >= 96 && tid < 96 + NF) tcnt[tid - 96] = d.nt ? d.ro.tq_cnt[jt * NF + tid - 96] : 0;
+    __syncthreads();
+    {
+        int lpre[MAX_J + 1], tpre[NF + 1];
+        lpre[0] = 0;
+#pragma unroll
+        for (int l = 0; l < MAX_J; l++) lpre[l + 1] = lpre[l] + (l < NJ ? lcnt[l] : 0);
+        tpre[0] = 0;
+#pragma unroll
+        for (int j = 0; j < NF; j++) tpre[j + 1] = tpre[j] + tcnt[j];
+        const int L = lpre[MAX_J], M = tpre[NF];
+        for (int u = tid; u < L + M; u += blockDim.x) {
+            if (u < L) {
+                int l = 0, q0 = 0;
+#pragma unroll
+                for (int k = 1; k < MAX_J; k++) if (u >= lpre[k]) { l = k; q0 = lpre[k]; }
+                const int q = u - q0;
+                const long b = (jt * NJ + l) * CAP_LM + q;
+                lh[l][q] = d.ro.link_hash[b];
+                lco[l][q][0] = d.ro.link_coef[b * 3];
+                lco[l][q][1] = d.ro.link_coef[b * 3 + 1];
+                lco[l][q][2] = d.ro.link_coef[b * 3 + 2];
+            } else {
+                const int v = u - L;
+                int j = 0, q0 = 0;
+#pragma unroll
+                for (int k = 1; k < NF; k++) if (v >= tpre[k]) { j = k; q0 = tpre[k]; }
+                const int q = v - q0;
+                const long b = (jt * NF + j) * CAP_UM + q;
+                th[j][q] = d.ro.tq_hash[b];
+                tco[j][q] = d.ro.tq_coef[b];
+            }
+        }
+    }
+    __syncthreads();
+    // value slices of every trial: link centres (k, l, e) and torque rows (k, j), monomial order
+    auto vterm = [&](double co, int h, int kk) {
+        double v = co;
+#pragma unroll
+        for (int j = 0; j < NF; j++) v = v * ptab[kk][j][(h >> (2 * j)) & 3];
+        return v;
+    };
+    const int nlv = K * NJ * 3, ntv = d.nt ? K * NF : 0;
+    for (int u = tid; u < nlv + ntv; u += blockDim.x) {
+        if (u < nlv) {
+            const int kk = u / (NJ * 3), l = (u / 3) % NJ, e = u % 3;
+            const long base = jt * NJ + l;
+            double c = d.ro.link_center[base * 3 + e];
+            const int cnt = lcnt[l];
+            int q = 0;
+            for (; q + 4 <= cnt; q += 4) {
+                const double v0 = vterm(lco[l][q][e], lh[l][q], kk), v1 = vterm(lco[l][q + 1][e], lh[l][q + 1], kk);
+                const double v2 = vterm(lco[l][q + 2][e], lh[l][q + 2], kk), v3 = vterm(lco[l][q + 3][e], lh[l][q + 3], kk);
+                c = c + v0; c = c + v1; c = c + v2; c = c + v3;
+            }
+            for (; q < cnt; q++) c = c + vterm(lco[l][q][e], lh[l][q], kk);
+            const double r = d.ro.link_rad[base * 3 + e];
+            lck[kk][l][e] = ((c - r) + (c + r)) * 0.5;  // getCenter(Interval(c - r, c + r))
+        } else {
+            const int v = u - nlv, kk = v / NF, j = v % NF;
+            const long base = jt * NF + j;
+            double c = d.ro.tq_center[base];
+            const int cnt = tcnt[j];
+            int q = 0;
+            for (; q + 4 <= cnt; q += 4) {
+                const double v0 = vterm(tco[j][q], th[j][q], kk), v1 = vterm(tco[j][q + 1], th[j][q + 1], kk);
+                const double v2 = vterm(tco[j][q + 2], th[j][q + 2], kk), v3 = vterm(tco[j][q + 3], th[j][q + 3], kk);
+                c = c + v0; c = c + v1; c = c + v2; c = c + v3;
+            }
+            for (; q < cnt; q++) c = c + vterm(tco[j][q], th[j][q], kk);
+            const double r = d.ro.tq_rad[base];
+            d.gs[((long)i * K + kk) * d.m + (long)t * NF + j] = ((c - r) + (c + r)) * 0.5;
+        }
+    }
+    if (t == 0 && tid >= (int)blockDim.x - K) {
+        // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267) of trial kk
+        const int kk = tid - ((int)blockDim.x - K);
+        const double* x = xk[kk];
+        double* const Gb = d.gs + ((long)i * K + kk) * d.m;
+        const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
+        const double* q0 = d.q0 + w * NF;
+        const double* qd0 = d.qd0 + w * NF;
+        const double* qdd0 = d.qdd0 + w * NF;
+        const double D = rp.duration;
+        for (int kind = 0; kind < 2; kind++)
+            for (int j = 0; j < NF; j++) {
+                double mn, mx, e2, e3;
+                int mnid, mxid;
+                extremum(kind, q0[j], qd0[j] * D, qdd0[j] * D * D, rp.k_range[j] * x[j], &mn, &mx, &mnid, &mxid, &e2, &e3);
+                const double scale = kind == 0 ? 1.0 : D;
+                const long rmin = off2 + kind * 2 * NF + j;
+                Gb[rmin] = mn / scale;
+                Gb[rmin + NF] = mx / scale;
+            }
+        const double tp = rp.t_plan;
+        double qp[NF];
+        for (int j = 0; j < NF; j++) qp[j] = bz_q(q0[j], qd0[j] * D, qdd0[j] * D * D, rp.k_range[j] * x[j], tp);
+        double fv = 0.0;
+        bool first = true;
+        for (int pass = 1; pass >= 0; pass--)
+            for (int j = 0; j < NF; j++) {
+                if (rp.wrap_mask[j] != pass) continue;
+                const double dd = pass ? wrap_to_pi(d.qdes[w * NF + j] - qp[j]) : (d.qdes[w * NF + j] - qp[j]);
+                const double term = dd * dd;
+                fv = first ? term : fv + term;
+                first = false;
+            }
+        d.fs[(long)i * K + kk] = fv * rp.cost_scale;
+    }
+    __syncthreads();
+    // collision rows of every trial from the plane cache: each pair's kept planes scanned once per
+    // trial, in order (first maximum, strict >), the records staged in LDS chunks
+    constexpr int PPT = (MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS;
+    constexpr int PC_CH = (MAX_J * CAP_LM * 3 + NF * CAP_UM) / 5;
+    double* const Sr = ubuf;
+    const double* const rec = d.pc + jt * 5 * d.pc_cap;
+    const int cap = d.pc_cap;
+    const unsigned* const po = d.pcoff + jt * NP;
+    const unsigned last = NP > 0 ? po[NP - 1] : 0u;
+    const int total = (int)(last >> 8) + (int)(last & 255);
+    int q0[PPT], n[PPT];
+    double best[PPT][EV_MAXK];
+#pragma unroll
+    for (int kp = 0; kp < PPT; kp++) {
+        const int pr = tid + kp * EVAL_THREADS;
+        const unsigned v = pr < NP ? po[pr] : 0u;
+        q0[kp] = (int)(v >> 8);
+        n[kp] = (int)(v & 255);
+#pragma unroll
+        for (int kk = 0; kk < EV_MAXK; kk++) best[kp][kk] = -100000000.0;
+    }
+    for (int r0 = 0; r0 < total; r0 += PC_CH) {
+        const int m = total - r0 < PC_CH ? total - r0 : PC_CH;
+        __syncthreads();
+        for (int u = tid; u < m; u += blockDim.x) {
+            const double a0 = rec[r0 + u], a1 = rec[cap + r0 + u], a2 = rec[2 * cap + r0 + u];
+            const double a3 = rec[3 * cap + r0 + u], a4 = rec[4 * cap + r0 + u];
+            Sr[u] = a0; Sr[PC_CH + u] = a1; Sr[2 * PC_CH + u] = a2; Sr[3 * PC_CH + u] = a3; Sr[4 * PC_CH + u] = a4;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kp = 0; kp < PPT; kp++) {
+            const int pr = tid + kp * EVAL_THREADS;
+            if (pr >= NP) continue;
+            const int l = pr / O;
+            const int lo = (q0[kp] > r0 ? q0[kp] : r0) - r0, hi = (q0[kp] + n[kp] < r0 + m ? q0[kp] + n[kp] : r0 + m) - r0;
+            for (int q = lo; q < hi; q++) {
+                const double A0 = Sr[q], A1 = Sr[PC_CH + q], A2 = Sr[2 * PC_CH + q];
+                const double P = Sr[3 * PC_CH + q], N = Sr[4 * PC_CH + q];
+#pragma unroll
+                for (int kk = 0; kk < EV_MAXK; kk++) {
+                    if (kk >= K) break;
+                    const double Ac = A0 * lck[kk][l][0] + A1 * lck[kk][l][1] + A2 * lck[kk][l][2];
+                    const double pos = Ac - P;
+                    const double neg = -Ac - N;
+                    if (pos > best[kp][kk]) best[kp][kk] = pos;
+                    if (neg > best[kp][kk]) best[kp][kk] = neg;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int kp = 0; kp < PPT; kp++) {
+        const int pr = tid + kp * EVAL_THREADS;
+        if (pr >= NP) continue;
+        const int l = pr / O, o = pr % O;
+        const long row = nt + ((long)l * d.T + t) * O + o;
+#pragma unroll
+        for (int kk = 0; kk < EV_MAXK; kk++)
+            if (kk < K) d.gs[((long)i * K + kk) * d.m + row] = -best[kp][kk];
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM
@@ -1524,47 +1726,6 @@ __global__ void ipm_world_Cs(NlpDev d) {
         }
     }
     if (threadIdx.x == 0) S.spec_k = chosen;
-}
-
-// the chosen trial's g, J, link centres, f and gradient into the world's trial slot
-__global__ void ipm_copy_spec(NlpDev d) {
-    const int w = d.wl[blockIdx.y];
-    const WorldState& S = d.ws[w];
-    if (S.spec_k < 0) return;
-    const long sidx = (long)blockIdx.y * d.K + S.spec_k;
-    const int slot = 1 - S.cur;
-    const long nlc = (long)d.T * d.NJ * 3, nc = (long)d.T * d.NJ * d.O;
-    const long nj0 = (long)d.nt * NF, nj1 = (d.m - d.nt - nc) * NF;  // dense J rows: before / after the collision rows
-    const long njn = nc * 3, njd = (long)d.T * d.NJ * NF * 3;
-    const long n = d.m + nj0 + nj1 + njn + njd + nlc;
-    double* g = d.g + gidx(d, slot, w, 0);
-    double* J = d.J + gidx(d, slot, w, 0) * NF;
-    double* jn = d.jn + slot * d.njn + (long)w * njn;
-    double* jd = d.jd + slot * d.njd + (long)w * njd;
-    double* lc = d.link_c + slot * d.lcs + (long)w * nlc;
-    const double* gs = d.gs + sidx * d.m;
-    const double* Js = d.Js + sidx * d.m * NF;
-    const double* jns = d.jns + sidx * njn;
-    const double* jds = d.jds + sidx * njd;
-    const double* ls = d.lcs_s + sidx * nlc;
-    for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
-        long u = q;
-        if (u < d.m) { g[u] = gs[u]; continue; }
-        u -= d.m;
-        if (u < nj0) { J[u] = Js[u]; continue; }
-        u -= nj0;
-        if (u < nj1) { J[(d.nt + nc) * NF + u] = Js[(d.nt + nc) * NF + u]; continue; }
-        u -= nj1;
-        if (u < njn) { jn[u] = jns[u]; continue; }
-        u -= njn;
-        if (u < njd) { jd[u] = jds[u]; continue; }
-        u -= njd;
-        lc[u] = ls[u];
-    }
-    if (blockIdx.x == 0 && threadIdx.x < NF) {
-        d.grad[((long)slot * d.W + w) * NF + threadIdx.x] = d.grads[sidx * NF + threadIdx.x];
-        if (threadIdx.x == 0) d.f[slot * d.W + w] = d.fs[sidx];
-    }
 }
 
 // pass D: accept the trial point — slacks, multipliers, BFGS ingredients

@@ -363,24 +363,22 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
     // active-world lists: two per iteration (ping-pong), two per line-search round
     if ((rc = p->alloc(&p->d_lists, 4 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 8))) return rc;
-    // speculative line-search slots: NSPEC worlds x (max_ls - 1) trials
-    d.K = d.opt.max_ls - 1;
-    p->spec = !std::getenv("ARMOUR_NO_SPEC") && d.K > 0;
-    if (p->spec) {
-        const size_t ns = (size_t)std::min(Wm, NSPEC) * d.K;
-        if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.Js, ns * mmax * NF)) || (rc = p->alloc(&d.fs, ns)) ||
-            (rc = p->alloc(&d.grads, ns * NF)) || (rc = p->alloc(&d.lcs_s, ns * T * NJ * 3)) ||
-            (rc = p->alloc(&d.jns, ns * T * NJ * Om * 3)) || (rc = p->alloc(&d.jds, ns * T * NJ * NF * 3)) ||
-            (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
-            return rc;
-    }
-    // certified plane cache: PC_AVG records per (link, obstacle) pair of every (world, t)
+    // certified plane cache: room for all 36 planes of every (link, obstacle) pair of every (world, t)
     d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
     d.pcready = 0;
     d.pc_cap = PC_K * NJ * Om;
     if (d.pcache && ((rc = p->alloc(&d.pc, jobs * 5 * (size_t)d.pc_cap)) || (rc = p->alloc(&d.pcoff, jobs * NJ * (size_t)Om)) ||
                      (rc = p->alloc(&d.pcok, jobs))))
         return rc;
+    // speculative line-search slots (values only): every world x (max_ls - 1) trials. The speculative
+    // round reads the plane cache (ARMOUR planner, fp64); otherwise the rounds run one by one.
+    d.K = d.opt.max_ls - 1;
+    p->spec = !std::getenv("ARMOUR_NO_SPEC") && d.K > 0 && d.K <= EV_MAXK && d.pcache && !p->armtd && !p->eval_f32;
+    if (p->spec) {
+        const size_t ns = (size_t)Wm * d.K;
+        if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.fs, ns)) || (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
+            return rc;
+    }
     HIPCK(hipMemset(d.cnt, 0, 8 * sizeof(unsigned)));
     d.lcount = nullptr;
     d.lcount_out = nullptr;
@@ -636,14 +634,15 @@ static int run_solver(armour_planner* p) {
             nnext = ((volatile int*)p->h_flags)[0];
             nsearch = ((volatile int*)p->h_flags)[1];
         }
-        if (nsearch > 0 && nsearch <= NSPEC && p->spec) {
+        if (nsearch > 0 && p->spec && d.pcready) {
+            // the worlds still searching: the values of all remaining trials at once, the acceptance
+            // tests in trial order, then the chosen trial in full
             NlpDev ds = d;
             ds.wl = Ls[1];
-            const int ny = nsearch * d.K;
-            launch_eval(p, dim3(p->T, ny), ds, 3);
-            hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, ny), dim3(ROW_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(eval_trials_kernel, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nsearch * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nsearch), dim3(64), 0, p->stream, ds);
-            hipLaunchKernelGGL(ipm_copy_spec, dim3(64, nsearch), dim3(256), 0, p->stream, ds);
+            launch_eval(p, dim3(p->T, nsearch), ds, 5);
         } else if (nsearch > 0) {
             for (int ls = 1; ls < d.opt.max_ls; ls++) {
                 NlpDev dc = d;
