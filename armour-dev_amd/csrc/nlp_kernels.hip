@@ -1039,6 +1039,9 @@ template __global__ void eval_kernel_t<double, true, true>(NlpDev, int);
 // acceptance test reads (ipm_rows_Cs / ipm_world_Cs); the Jacobian is formed only for the trial
 // chosen, by a full evaluation (eval_kernel_t mode 5). The monomials and the certified-plane
 // records are staged once for all K points; every value is formed with eval_kernel_t's arithmetic.
+// IPT: (trial, pair) items per thread, >= ceil(K * NJ * O / EVAL_THREADS) (planner.hip picks the
+// instantiation: 6 covers K = 9 trials of up to 170 pairs, e.g. 7 links x 20 obstacles)
+template <int IPT>
 __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
     const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
     const WorldState& S = d.ws[w];
@@ -1176,9 +1179,9 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
         d.fs[(long)i * K + kk] = fv * rp.cost_scale;
     }
     __syncthreads();
-    // collision rows of every trial from the plane cache: each pair's kept planes scanned once per
-    // trial, in order (first maximum, strict >), the records staged in LDS chunks
-    constexpr int PPT = (MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS;
+    // collision rows of every trial from the plane cache: one item per (trial, pair) scans the pair's
+    // kept planes in order (first maximum, strict >); the records staged in LDS chunks, each item's
+    // running maximum kept across chunks
     constexpr int PC_CH = (MAX_J * CAP_LM * 3 + NF * CAP_UM) / 5;
     double* const Sr = ubuf;
     const double* const rec = d.pc + jt * 5 * d.pc_cap;
@@ -1186,16 +1189,19 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
     const unsigned* const po = d.pcoff + jt * NP;
     const unsigned last = NP > 0 ? po[NP - 1] : 0u;
     const int total = (int)(last >> 8) + (int)(last & 255);
-    int q0[PPT], n[PPT];
-    double best[PPT][EV_MAXK];
+    const int nitem = K * NP;
+    int q0[IPT], n[IPT];
+    double best[IPT], c0[IPT], c1[IPT], c2[IPT];
 #pragma unroll
-    for (int kp = 0; kp < PPT; kp++) {
-        const int pr = tid + kp * EVAL_THREADS;
-        const unsigned v = pr < NP ? po[pr] : 0u;
-        q0[kp] = (int)(v >> 8);
-        n[kp] = (int)(v & 255);
-#pragma unroll
-        for (int kk = 0; kk < EV_MAXK; kk++) best[kp][kk] = -100000000.0;
+    for (int s = 0; s < IPT; s++) {
+        const int u = tid + s * EVAL_THREADS;
+        const int kk = u / (NP > 0 ? NP : 1), pr = u - kk * NP;
+        const unsigned v = u < nitem ? po[pr] : 0u;
+        q0[s] = (int)(v >> 8);
+        n[s] = (int)(v & 255);
+        best[s] = -100000000.0;
+        const int l = u < nitem ? pr / O : 0, kc = u < nitem ? kk : 0;
+        c0[s] = lck[kc][l][0]; c1[s] = lck[kc][l][1]; c2[s] = lck[kc][l][2];
     }
     for (int r0 = 0; r0 < total; r0 += PC_CH) {
         const int m = total - r0 < PC_CH ? total - r0 : PC_CH;
@@ -1207,37 +1213,29 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
         }
         __syncthreads();
 #pragma unroll
-        for (int kp = 0; kp < PPT; kp++) {
-            const int pr = tid + kp * EVAL_THREADS;
-            if (pr >= NP) continue;
-            const int l = pr / O;
-            const int lo = (q0[kp] > r0 ? q0[kp] : r0) - r0, hi = (q0[kp] + n[kp] < r0 + m ? q0[kp] + n[kp] : r0 + m) - r0;
+        for (int s = 0; s < IPT; s++) {
+            const int lo = (q0[s] > r0 ? q0[s] : r0) - r0, hi = (q0[s] + n[s] < r0 + m ? q0[s] + n[s] : r0 + m) - r0;
             for (int q = lo; q < hi; q++) {
-                const double A0 = Sr[q], A1 = Sr[PC_CH + q], A2 = Sr[2 * PC_CH + q];
-                const double P = Sr[3 * PC_CH + q], N = Sr[4 * PC_CH + q];
-#pragma unroll
-                for (int kk = 0; kk < EV_MAXK; kk++) {
-                    if (kk >= K) break;
-                    const double Ac = A0 * lck[kk][l][0] + A1 * lck[kk][l][1] + A2 * lck[kk][l][2];
-                    const double pos = Ac - P;
-                    const double neg = -Ac - N;
-                    if (pos > best[kp][kk]) best[kp][kk] = pos;
-                    if (neg > best[kp][kk]) best[kp][kk] = neg;
-                }
+                const double Ac = Sr[q] * c0[s] + Sr[PC_CH + q] * c1[s] + Sr[2 * PC_CH + q] * c2[s];
+                const double pos = Ac - Sr[3 * PC_CH + q];
+                const double neg = -Ac - Sr[4 * PC_CH + q];
+                if (pos > best[s]) best[s] = pos;
+                if (neg > best[s]) best[s] = neg;
             }
         }
     }
 #pragma unroll
-    for (int kp = 0; kp < PPT; kp++) {
-        const int pr = tid + kp * EVAL_THREADS;
-        if (pr >= NP) continue;
+    for (int s = 0; s < IPT; s++) {
+        const int u = tid + s * EVAL_THREADS;
+        if (u >= nitem) continue;
+        const int kk = u / NP, pr = u - kk * NP;
         const int l = pr / O, o = pr % O;
-        const long row = nt + ((long)l * d.T + t) * O + o;
-#pragma unroll
-        for (int kk = 0; kk < EV_MAXK; kk++)
-            if (kk < K) d.gs[((long)i * K + kk) * d.m + row] = -best[kp][kk];
+        d.gs[((long)i * K + kk) * d.m + nt + ((long)l * d.T + t) * O + o] = -best[s];
     }
 }
+
+template __global__ void eval_trials_kernel<6>(NlpDev);
+template __global__ void eval_trials_kernel<(EV_MAXK * MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS>(NlpDev);
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM
