@@ -1589,7 +1589,14 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
     block_reduce_n(v, kinds, lds, out);
 }
 
-__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft);
+__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft, bool filt);
+// the filter test of a trial (theta_t, phi_t) on a whole wave, one filter entry per lane
+// (MAX_FILTER <= 64): acceptable to the filter iff no entry dominates it
+__device__ inline bool filter_pass(const WorldState& S, double thetat, double phit) {
+    const int q = threadIdx.x & 63;
+    const bool fail = q < S.nfilt && !(thetat < S.filt_theta[q] || phit < S.filt_phi[q]);
+    return __ballot(fail) == 0;
+}
 __device__ inline void world_C_body(const NlpDev& d, int w) {
     WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
@@ -1597,18 +1604,18 @@ __device__ inline void world_C_body(const NlpDev& d, int w) {
     const double init[2] = {0.0, 0.0};
     const int op[2] = {0, 0};
     world_partials(d, w, init, op, P);
+    const double ft = d.f[(1 - S.cur) * d.W + w];
+    const bool filt = filter_pass(S, P[1], ft - S.mu * P[0]);
     if (threadIdx.x != 0) return;
-    accept_trial(d, S, P[0], P[1], d.f[(1 - S.cur) * d.W + w]);
+    accept_trial(d, S, P[0], P[1], ft, filt);
 }
 
 // the filter acceptance test of one trial point (barrier terms logt, violation rpt, objective ft);
 // on failure the next trial (alpha halved) or, after max_ls trials, the forced last one
-__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft) {
+__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft, bool filt) {
     S.nevals++;
     const double phit = ft - S.mu * logt, thetat = rpt;
-    bool ok = thetat <= S.theta_max;
-    for (int q = 0; ok && q < S.nfilt; q++)
-        if (!(thetat < S.filt_theta[q] || phit < S.filt_phi[q])) ok = false;
+    bool ok = thetat <= S.theta_max && filt;  // filt: filter_pass of (thetat, phit)
     bool ftype = false;
     if (ok) {
         const bool switching = S.Dphi < 0 && S.alpha * S.sw_dphi > S.sw_theta;
@@ -1712,14 +1719,19 @@ __global__ void ipm_world_Cs(NlpDev d) {
     }
     const uint64_t u = __builtin_bit_cast(uint64_t, s);
     int chosen = -1;
+    const double mu = S.mu;
     for (int k = 0; k < d.K; k++) {
         const uint32_t lo0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 2 * k);
         const uint32_t hi0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 2 * k);
         const uint32_t lo1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 2 * k + 1);
         const uint32_t hi1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 2 * k + 1);
+        const double logt = __builtin_bit_cast(double, ((uint64_t)hi0 << 32) | lo0);
+        const double rpt = __builtin_bit_cast(double, ((uint64_t)hi1 << 32) | lo1);
+        const double ft = d.fs[(long)i * d.K + k];
+        // (the filter does not change while a search goes on: an acceptance ends it)
+        const bool filt = filter_pass(S, rpt, ft - mu * logt);
         if (threadIdx.x == 0 && chosen == k - 1 && S.status == 0 && S.searching) {
-            accept_trial(d, S, __builtin_bit_cast(double, ((uint64_t)hi0 << 32) | lo0),
-                         __builtin_bit_cast(double, ((uint64_t)hi1 << 32) | lo1), d.fs[(long)i * d.K + k]);
+            accept_trial(d, S, logt, rpt, ft, filt);
             chosen = k;
         }
     }
