@@ -8,6 +8,7 @@ constexpr int EVAL_THREADS = 256;
 constexpr int ROW_THREADS = 256;
 constexpr int MAX_FILTER = 64;
 constexpr int KA = 56;   // partial-sum slots per row block (pass A is the largest user)
+constexpr int KA2 = 8;   // pass D's partial sums (partial2), kept apart so the fused D + A pass writes both
 
 // solver options (oracle/src/ipm.h IpmOptions)
 struct IpmOpts {
@@ -81,6 +82,7 @@ struct NlpDev {
     // solver row state [W][R]
     double *slo, *shi, *zlo, *zhi, *dslo, *dshi, *dzlo, *dzhi, *rplo, *rphi;
     double* partial;        // [W][nblk][KA]
+    double* partial2;       // [W][nblk][KA2]: pass D
     WorldState* ws;         // [W]
     int* flags;             // mapped host memory: [0] worlds running (round 0 of an iteration),
                             // [1] worlds still searching after the last line-search round

@@ -1239,7 +1239,7 @@ template __global__ void eval_trials_kernel<(EV_MAXK * MAX_J * MAX_OBS + EVAL_TH
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM
-__global__ void ipm_world_init(NlpDev d) {
+__global__ __launch_bounds__(64) void ipm_world_init(NlpDev d) {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= d.W) return;
     WorldState& S = d.ws[w];
@@ -1295,17 +1295,102 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
 }
 
 // pass A: residuals, errors, reduced Newton system sums
+// pass A's row accumulation (residuals, Newton system) at the current point: value v, gradient a
+struct AAcc {
+    double rdp[NF], M[28], u1[NF], u2[NF];
+    double inf_p, compl0, cm, sumz;
+    __device__ void zero() {
+#pragma unroll
+        for (int j = 0; j < NF; j++) { rdp[j] = 0; u1[j] = 0; u2[j] = 0; }
+#pragma unroll
+        for (int k = 0; k < 28; k++) M[k] = 0;
+        inf_p = 0; compl0 = 0; cm = 0; sumz = 0;
+    }
+};
+__device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, long i, double v, const double* a, double L,
+                                                            double U, double mu, AAcc& c) {
+    double wr = 0, sig = 0, c1 = 0, c2 = 0;
+    if (has_lo(d, L)) {
+        const double s = d.slo[i], z = d.zlo[i];
+        const double rp = (v - L) - s;
+        d.rplo[i] = rp;
+        wr += z;
+        c.inf_p = fmax(c.inf_p, fabs(rp));
+        c.compl0 = fmax(c.compl0, s * z);
+        c.cm = fmax(c.cm, fabs(s * z - mu));
+        c.sumz += z;
+        const double sg = z / s;
+        sig += sg;
+        c1 += 1.0 / s;
+        c2 += sg * rp;
+    }
+    if (has_hi(d, U)) {
+        const double s = d.shi[i], z = d.zhi[i];
+        const double rp = (U - v) - s;
+        d.rphi[i] = rp;
+        wr -= z;
+        c.inf_p = fmax(c.inf_p, fabs(rp));
+        c.compl0 = fmax(c.compl0, s * z);
+        c.cm = fmax(c.cm, fabs(s * z - mu));
+        c.sumz += z;
+        const double sg = z / s;
+        sig += sg;
+        c1 -= 1.0 / s;
+        c2 -= sg * rp;
+    }
+    int k = 0;
+#pragma unroll
+    for (int p = 0; p < NF; p++) {
+        c.rdp[p] += wr * a[p];
+        c.u1[p] += a[p] * c1;
+        c.u2[p] += a[p] * c2;
+#pragma unroll
+        for (int q = p; q < NF; q++) c.M[k++] += sig * a[p] * a[q];
+    }
+}
+__device__ inline void reduce_A(const NlpDev& d, int w, AAcc& c, double* lds) {
+    double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
+    double v[53];
+    int kinds[53];
+#pragma unroll
+    for (int j = 0; j < NF; j++) { v[j] = c.rdp[j]; v[39 + j] = c.u1[j]; v[46 + j] = c.u2[j]; }
+    v[7] = c.inf_p; v[8] = c.compl0; v[9] = c.cm; v[10] = c.sumz;
+#pragma unroll
+    for (int k = 0; k < 28; k++) v[11 + k] = c.M[k];
+#pragma unroll
+    for (int k = 0; k < 53; k++) kinds[k] = (k >= 7 && k <= 9) ? 1 : 0;
+    block_reduce_n(v, kinds, lds, out);
+}
+// pass D's row update (accept the trial: slacks, multipliers) and the BFGS ingredient sum w a
+__device__ inline __attribute__((always_inline)) void row_D(const NlpDev& d, long i, const double* a, double L, double U,
+                                                            double mu, double ad, double alpha, double* wn) {
+    const double ks = d.opt.kappa_sigma;
+    double wv = 0;
+    if (has_lo(d, L)) {
+        const double zn = d.zlo[i] + ad * d.dzlo[i];
+        wv += zn;
+        const double s = d.slo[i] + alpha * d.dslo[i];
+        d.slo[i] = s;
+        d.zlo[i] = fmin(fmax(zn, mu / (ks * s)), ks * mu / s);
+    }
+    if (has_hi(d, U)) {
+        const double zn = d.zhi[i] + ad * d.dzhi[i];
+        wv -= zn;
+        const double s = d.shi[i] + alpha * d.dshi[i];
+        d.shi[i] = s;
+        d.zhi[i] = fmin(fmax(zn, mu / (ks * s)), ks * mu / s);
+    }
+#pragma unroll
+    for (int j = 0; j < NF; j++) wn[j] += wv * a[j];
+}
+
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
     __shared__ double lds[(ROW_THREADS / 64) * 53];
-    double rdp[NF], M[28], u1[NF], u2[NF];
-    double inf_p = 0, compl0 = 0, cm = 0, sumz = 0;
-#pragma unroll
-    for (int j = 0; j < NF; j++) { rdp[j] = 0; u1[j] = 0; u2[j] = 0; }
-#pragma unroll
-    for (int k = 0; k < 28; k++) M[k] = 0;
+    AAcc c;
+    c.zero();
     const double mu = S.mu;
     const long r0 = (long)blockIdx.x * d.chunk;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
@@ -1314,56 +1399,39 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
         const long i = (long)w * d.R + r;
         double L, U;
         row_bounds(d, i, (int)r, L, U);
-        double wr = 0, sig = 0, c1 = 0, c2 = 0;
-        if (has_lo(d, L)) {
-            const double s = d.slo[i], z = d.zlo[i];
-            const double rp = (v - L) - s;
-            d.rplo[i] = rp;
-            wr += z;
-            inf_p = fmax(inf_p, fabs(rp));
-            compl0 = fmax(compl0, s * z);
-            cm = fmax(cm, fabs(s * z - mu));
-            sumz += z;
-            const double sg = z / s;
-            sig += sg;
-            c1 += 1.0 / s;
-            c2 += sg * rp;
-        }
-        if (has_hi(d, U)) {
-            const double s = d.shi[i], z = d.zhi[i];
-            const double rp = (U - v) - s;
-            d.rphi[i] = rp;
-            wr -= z;
-            inf_p = fmax(inf_p, fabs(rp));
-            compl0 = fmax(compl0, s * z);
-            cm = fmax(cm, fabs(s * z - mu));
-            sumz += z;
-            const double sg = z / s;
-            sig += sg;
-            c1 -= 1.0 / s;
-            c2 -= sg * rp;
-        }
-        int k = 0;
-#pragma unroll
-        for (int p = 0; p < NF; p++) {
-            rdp[p] += wr * a[p];
-            u1[p] += a[p] * c1;
-            u2[p] += a[p] * c2;
-#pragma unroll
-            for (int q = p; q < NF; q++) M[k++] += sig * a[p] * a[q];
-        }
+        row_A(d, i, v, a, L, U, mu, c);
     }
-    double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
-    double v[53];
-    int kinds[53];
+    reduce_A(d, w, c, lds);
+}
+
+// passes D (of the previous iteration) and A (of this one) in one sweep over the rows: the trial
+// point D accepts is the point A works at, so each row's value and gradient are read once; the
+// arithmetic of ipm_rows_D then ipm_rows_A. D's sums go to partial2, A's to partial.
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
+    const int w = world_of(d, blockIdx.y);
+    const WorldState& S = d.ws[w];
+    if (S.status != 0) return;
+    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    const double mu = S.mu, ad = S.ad, alpha = S.alpha;
+    double wn[NF];
 #pragma unroll
-    for (int j = 0; j < NF; j++) { v[j] = rdp[j]; v[39 + j] = u1[j]; v[46 + j] = u2[j]; }
-    v[7] = inf_p; v[8] = compl0; v[9] = cm; v[10] = sumz;
-#pragma unroll
-    for (int k = 0; k < 28; k++) v[11 + k] = M[k];
-#pragma unroll
-    for (int k = 0; k < 53; k++) kinds[k] = (k >= 7 && k <= 9) ? 1 : 0;
-    block_reduce_n(v, kinds, lds, out);
+    for (int j = 0; j < NF; j++) wn[j] = 0;
+    AAcc c;
+    c.zero();
+    const long r0 = (long)blockIdx.x * d.chunk;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        double a[NF];
+        const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
+        const long i = (long)w * d.R + r;
+        double L, U;
+        row_bounds(d, i, (int)r, L, U);
+        row_D(d, i, a, L, U, mu, ad, alpha, wn);
+        row_A(d, i, v, a, L, U, mu, c);
+    }
+    const int kinds[NF] = {};
+    block_reduce_n(wn, kinds, lds, d.partial2 + ((long)w * d.nblk + blockIdx.x) * KA2);
+    __syncthreads();
+    reduce_A(d, w, c, lds);
 }
 
 __device__ bool chol_solve7(const double* M, double shift, const double* b, double* x) {
@@ -1398,15 +1466,15 @@ __device__ bool chol_solve7(const double* M, double shift, const double* b, doub
 // onto init. The per-world kernels run one wave per world: the nblk dependent load rounds of a
 // single thread become one round per lane.
 template <int N>
-__device__ inline void world_partials_at(const double* base, int nblk, const double (&init)[N], const int (&op)[N],
-                                         double (&P)[N]);
+__device__ inline void world_partials_at(const double* base, int nblk, int stride, const double (&init)[N],
+                                         const int (&op)[N], double (&P)[N]);
 template <int N>
 __device__ inline void world_partials(const NlpDev& d, int w, const double (&init)[N], const int (&op)[N], double (&P)[N]) {
-    world_partials_at(d.partial + (long)w * d.nblk * KA, d.nblk, init, op, P);
+    world_partials_at(d.partial + (long)w * d.nblk * KA, d.nblk, KA, init, op, P);
 }
 template <int N>
-__device__ inline void world_partials_at(const double* base, int nblk, const double (&init)[N], const int (&op)[N],
-                                         double (&P)[N]) {
+__device__ inline void world_partials_at(const double* base, int nblk, int stride, const double (&init)[N],
+                                         const int (&op)[N], double (&P)[N]) {
     const int lane = threadIdx.x & 63;
     double s = 0;
     int o = 0;
@@ -1416,7 +1484,7 @@ __device__ inline void world_partials_at(const double* base, int nblk, const dou
     if (lane < N) {
         const double* in = base + lane;
         for (int b = 0; b < nblk; b++) {
-            const double x = in[(long)b * KA];
+            const double x = in[(long)b * stride];
             s = o == 0 ? s + x : o == 1 ? fmax(s, x) : fmin(s, x);
         }
     }
@@ -1429,8 +1497,10 @@ __device__ inline void world_partials_at(const double* base, int nblk, const dou
     }
 }
 
-__global__ void ipm_world_A(NlpDev d, int nside) {
-    const int w = world_of(d, blockIdx.x);
+__device__ inline void world_A_body(const NlpDev& d, int w, int nside);
+__global__ __launch_bounds__(64) void ipm_world_A(NlpDev d, int nside) { world_A_body(d, world_of(d, blockIdx.x), nside); }
+// pass A's world step: convergence test, barrier update, Newton step; every lane of the wave calls it
+__device__ inline void world_A_body(const NlpDev& d, int w, int nside) {
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
     if (S.iter >= d.opt.max_iter) {  // oracle: loop ends without a final check
@@ -1533,7 +1603,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
     block_reduce_n(v, kinds, lds, out);
 }
 
-__global__ void ipm_world_B(NlpDev d) {
+__global__ __launch_bounds__(64) void ipm_world_B(NlpDev d) {
     const int w = world_of(d, blockIdx.x);
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
@@ -1651,7 +1721,7 @@ __device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt,
 // still running (round 0) and still searching are appended to the next lists (their order only
 // decides which block serves which world), and the last block to finish publishes both counts to
 // the mapped host flags and resets the counters for the next launch.
-__global__ void ipm_world_C(NlpDev d) {
+__global__ __launch_bounds__(64) void ipm_world_C(NlpDev d) {
     const bool valid = !d.lcount || blockIdx.x < *d.lcount;
     const int w = valid ? world_of(d, blockIdx.x) : 0;
     if (valid) world_C_body(d, w);
@@ -1708,7 +1778,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
 // (ipm_world_C): the first acceptable one ends the search, or the last (forced) one
 // list entry blockIdx.x (one wave): every trial's two partial sums at once (lane 2 k + q, block
 // partials summed in order as world_partials_at), then the acceptance tests in trial order on lane 0
-__global__ void ipm_world_Cs(NlpDev d) {
+__global__ __launch_bounds__(64) void ipm_world_Cs(NlpDev d) {
     const int i = blockIdx.x, w = d.wl[i];
     WorldState& S = d.ws[w];
     const int lane = threadIdx.x & 63;
@@ -1744,7 +1814,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
     __shared__ double lds[(ROW_THREADS / 64) * 53];
-    const double mu = S.mu, ad = S.ad, alpha = S.alpha, ks = d.opt.kappa_sigma;
+    const double mu = S.mu, ad = S.ad, alpha = S.alpha;
     double wn[NF];
 #pragma unroll
     for (int j = 0; j < NF; j++) wn[j] = 0;
@@ -1755,37 +1825,21 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
         const long i = (long)w * d.R + r;
         double L, U;
         row_bounds(d, i, (int)r, L, U);
-        double wv = 0;
-        if (has_lo(d, L)) {
-            const double zn = d.zlo[i] + ad * d.dzlo[i];
-            wv += zn;
-            const double s = d.slo[i] + alpha * d.dslo[i];
-            d.slo[i] = s;
-            d.zlo[i] = fmin(fmax(zn, mu / (ks * s)), ks * mu / s);
-        }
-        if (has_hi(d, U)) {
-            const double zn = d.zhi[i] + ad * d.dzhi[i];
-            wv -= zn;
-            const double s = d.shi[i] + alpha * d.dshi[i];
-            d.shi[i] = s;
-            d.zhi[i] = fmin(fmax(zn, mu / (ks * s)), ks * mu / s);
-        }
-#pragma unroll
-        for (int j = 0; j < NF; j++) wn[j] += wv * a[j];
+        row_D(d, i, a, L, U, mu, ad, alpha, wn);
     }
-    double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
+    double* out = d.partial2 + ((long)w * d.nblk + blockIdx.x) * KA2;
     const int kinds[NF] = {};
     block_reduce_n(wn, kinds, lds, out);
 }
 
-__global__ void ipm_world_D(NlpDev d) {
-    const int w = world_of(d, blockIdx.x);
+// pass D's world step: BFGS update, accept the trial point; every lane of the wave calls it
+__device__ inline void world_D_body(const NlpDev& d, int w) {
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
     double wn[NF];
     const double init[NF] = {};
     const int op[NF] = {};
-    world_partials(d, w, init, op, wn);
+    world_partials_at(d.partial2 + (long)w * d.nblk * KA2, d.nblk, KA2, init, op, wn);
     if (threadIdx.x != 0) return;
     const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
     const double* gradt = d.grad + ((long)(1 - S.cur) * d.W + w) * NF;
@@ -1823,6 +1877,15 @@ __global__ void ipm_world_D(NlpDev d) {
     S.nfail = S.accepted_ok ? 0 : S.nfail + 1;
     S.iter++;
     if (S.nfail >= 3) S.status = 3;
+}
+__global__ __launch_bounds__(64) void ipm_world_D(NlpDev d) { world_D_body(d, world_of(d, blockIdx.x)); }
+__device__ inline void world_A_body(const NlpDev& d, int w, int nside);
+// the fused passes' world step: D's (of the previous iteration), then A's, one wave
+__global__ __launch_bounds__(64) void ipm_world_DA(NlpDev d, int nside) {
+    const int w = world_of(d, blockIdx.x);
+    world_D_body(d, w);
+    __syncthreads();  // lane 0's WorldState stores before every lane's reads in world_A_body
+    world_A_body(d, w, nside);
 }
 
 // finalize_solution's feasibility re-check (NLPclass.cu:449-538): one block per world

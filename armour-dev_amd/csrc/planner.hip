@@ -354,7 +354,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     for (double** b : rowbufs)
         if ((rc = p->alloc(b, Wm * Rmax))) return rc;
     const int nblk_max = (int)((Rmax + row_chunk() - 1) / row_chunk());
-    if ((rc = p->alloc(&d.partial, (size_t)Wm * nblk_max * KA)) || (rc = p->alloc(&d.ws, (size_t)Wm)) ||
+    if ((rc = p->alloc(&d.partial, (size_t)Wm * nblk_max * KA)) || (rc = p->alloc(&d.partial2, (size_t)Wm * nblk_max * KA2)) ||
+        (rc = p->alloc(&d.ws, (size_t)Wm)) ||
         (rc = p->alloc(&p->feas, (size_t)Wm)))
         return rc;
     // the solver's two continue flags live in mapped host memory: kernels store 1 into them, the
@@ -610,8 +611,15 @@ static int run_solver(armour_planner* p) {
     for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
         NlpDev di = d;
         di.wl = Li[cur];
-        hipLaunchKernelGGL(ipm_rows_A, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
-        hipLaunchKernelGGL(ipm_world_A, dim3(nrun), dim3(64), 0, p->stream, di, ns);
+        // pass D of the previous iteration (accept its trial point) shares one sweep over the rows
+        // with this iteration's pass A
+        if (it == 0) {
+            hipLaunchKernelGGL(ipm_rows_A, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
+            hipLaunchKernelGGL(ipm_world_A, dim3(nrun), dim3(64), 0, p->stream, di, ns);
+        } else {
+            hipLaunchKernelGGL(ipm_rows_DA, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
+            hipLaunchKernelGGL(ipm_world_DA, dim3(nrun), dim3(64), 0, p->stream, di, ns);
+        }
         hipLaunchKernelGGL(ipm_rows_B, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
         hipLaunchKernelGGL(ipm_world_B, dim3(nrun), dim3(64), 0, p->stream, di);
         // Round 0 of the line search for every running world, then one host synchronisation. The
@@ -659,8 +667,6 @@ static int run_solver(armour_planner* p) {
             }
         }
         if (nnext == 0) break;  // every world converged, hit the cap or failed
-        hipLaunchKernelGGL(ipm_rows_D, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
-        hipLaunchKernelGGL(ipm_world_D, dim3(nrun), dim3(64), 0, p->stream, di);
         HIPCK(hipGetLastError());
         cur = 1 - cur;
         nrun = nnext;

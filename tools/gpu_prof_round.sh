@@ -15,7 +15,7 @@ timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/evaltrace -
 cd $R
 python3 tools/stats_summary.py $O/trace/run_kernel_stats.csv profiles/${RND}_kernel_stats.txt "rocprofv3 --kernel-trace --stats -- python3 bench.py (defaults), $RND" > /dev/null
 cp $O/trace/run_kernel_stats.csv profiles/${RND}_kernel_stats.csv
-tail -1 $O/trace.log > profiles/${RND}_bench_profiled.json
+grep "^{\"metric\"" $O/trace.log | tail -1 > profiles/${RND}_bench_profiled.json
 python3 tools/pmc_traffic.py $O/fetch/run_counter_collection.csv $O/write/run_counter_collection.csv lane_reach_kernel profiles/${RND}_reach_traffic.json $RND 327 survey > /dev/null
 python3 tools/eval_valu.py $O/evalpmc/run_counter_collection.csv $O/evaltrace/run_kernel_trace.csv profiles/${RND}_eval_valu.json > /dev/null
 mkdir -p gpurun_out/profiles_new && cp profiles/${RND}_* gpurun_out/profiles_new/
