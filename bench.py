@@ -53,9 +53,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=0,
                     help="worlds per planner per step (0: two whole bundle waves of the device, floor(2 * CUs * 64 / T): "
                          "327 on MI355X at T=100)")
-    ap.add_argument("--planners", type=int, default=2,
+    ap.add_argument("--planners", type=int, default=3,
                     help="planners per GPU planning their own batch concurrently (one HIP stream and one host thread "
-                         "each); 2 overlaps one planner's solver with the other's reach")
+                         "each): one planner's solver fills the GPU around the others' (DESIGN.md section 6: 3 "
+                         "measured best, 2 about 2.5 %% behind, 4 behind)")
     ap.add_argument("--total-worlds", type=int, default=0,
                     help="strong scaling (config 4): one job of this many worlds sharded over the ranks")
     ap.add_argument("--T", type=int, default=100)

@@ -1,5 +1,5 @@
 """Per-iteration time of the traced plan of tools/nlp_trace.py (rocprofv3 --kernel-trace CSV): the
-iterations start at each ipm_rows_A launch; prints worlds running, wall span and eval share per
+iterations start at each ipm_rows_A / ipm_rows_DA launch; prints worlds running, wall span and eval share per
 iteration bucket. Development tool. usage: iter_profile.py <kernel_trace.csv>"""
 import csv
 import sys
@@ -8,7 +8,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "reach_kernel" in r["Kernel_Name"]]
 R = rows[idx[-1] + 1:]
-its = [i for i, r in enumerate(R) if "ipm_rows_A" in r["Kernel_Name"]]
+its = [i for i, r in enumerate(R) if "ipm_rows_A" in r["Kernel_Name"] or "ipm_rows_DA" in r["Kernel_Name"]]
 its.append(len(R))
 out = []
 for a, b in zip(its[:-1], its[1:]):
