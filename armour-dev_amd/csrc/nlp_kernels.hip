@@ -1040,7 +1040,8 @@ template __global__ void eval_kernel_t<double, true, true>(NlpDev, int);
 // chosen, by a full evaluation (eval_kernel_t mode 5). The monomials and the certified-plane
 // records are staged once for all K points; every value is formed with eval_kernel_t's arithmetic.
 // IPT: (trial, pair) items per thread, >= ceil(K * NJ * O / EVAL_THREADS) (planner.hip picks the
-// instantiation: 6 covers K = 9 trials of up to 170 pairs, e.g. 7 links x 20 obstacles)
+// smallest instantiation: 6 covers K = 9 trials of up to 170 pairs, e.g. 7 links x 20 obstacles;
+// 10 up to 284, e.g. 7 x 40)
 template <int IPT>
 __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
     const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
@@ -1235,6 +1236,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
 }
 
 template __global__ void eval_trials_kernel<6>(NlpDev);
+template __global__ void eval_trials_kernel<10>(NlpDev);
 template __global__ void eval_trials_kernel<(EV_MAXK * MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS>(NlpDev);
 
 // ------------------------------------------------------------------------------------------

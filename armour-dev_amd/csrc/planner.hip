@@ -648,7 +648,9 @@ static int run_solver(armour_planner* p) {
             NlpDev ds = d;
             ds.wl = Ls[1];
             constexpr int IPT_MAX = (EV_MAXK * MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS;
-            auto tk = d.K * p->NJ * d.O <= 6 * EVAL_THREADS ? eval_trials_kernel<6> : eval_trials_kernel<IPT_MAX>;
+            const int items = d.K * p->NJ * d.O;
+            auto tk = items <= 6 * EVAL_THREADS ? eval_trials_kernel<6>
+                      : items <= 10 * EVAL_THREADS ? eval_trials_kernel<10> : eval_trials_kernel<IPT_MAX>;
             hipLaunchKernelGGL(tk, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nsearch * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nsearch), dim3(64), 0, p->stream, ds);
