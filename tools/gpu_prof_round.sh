@@ -22,3 +22,9 @@ mkdir -p gpurun_out/profiles_new && cp profiles/${RND}_* gpurun_out/profiles_new
 head -12 profiles/${RND}_kernel_stats.txt
 cat profiles/${RND}_reach_traffic.json | head -8
 python3 -c "import json; d=json.load(open('profiles/${RND}_eval_valu.json')); print({k: d[k] for k in ('fp64_tflops','frac_of_fp64_peak','valu_busy','median_duration_s')})"
+# solver timeline of one planner (one traced plan of the bench batch): per-iteration buckets and kernel totals
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/prof_$RND/nlp -o run -- python3 $R/tools/nlp_trace.py survey 327 > $R/gpurun_out/prof_$RND/nlp.log 2>&1 || { echo nlp trace failed; exit 1; }
+cd $R
+{ echo "# one planner, 327 survey worlds, T=100, O=20: rocprofv3 --kernel-trace -- python3 tools/nlp_trace.py survey 327 ($RND)"; python3 tools/iter_profile.py gpurun_out/prof_$RND/nlp/run_kernel_trace.csv; python3 tools/trace_summary.py gpurun_out/prof_$RND/nlp/run_kernel_trace.csv; } > profiles/${RND}_solver_timeline.txt
+cp profiles/${RND}_solver_timeline.txt gpurun_out/profiles_new/
+cat profiles/${RND}_solver_timeline.txt | head -8
