@@ -9,7 +9,7 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "reach_kernel" in r["Kernel_Name"]]
 R = rows[idx[-1]:]
 t0 = int(R[0]["Start_Timestamp"])
-names = ["eval_kernel", "ipm_rows_Cs", "ipm_world_Cs", "ipm_copy_spec", "ipm_rows_A", "ipm_rows_B", "ipm_rows_C",
+names = ["eval_kernel", "eval_trials_kernel", "ipm_world_Cs", "ipm_rows_A", "ipm_rows_DA", "ipm_rows_B",
          "ipm_rows_D", "ipm_world_A", "ipm_world_B", "ipm_world_C", "ipm_world_D", "lane_reach", "reach_kernel",
          "bounds", "feasible", "jrs", "ipm_world_init", "ipm_rows_init"]
 
