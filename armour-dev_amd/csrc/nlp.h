@@ -116,6 +116,7 @@ struct NlpDev {
     int pcready;            // built for the current reach sets and obstacles
     int pc_cap;             // records per (world, t)
     double* pc;
+    uint16_t* pcp;          // [W][T][pc_cap]: the pair (l * O + o) of each record
     unsigned* pcoff;
     unsigned char* pcok;
 };

@@ -406,6 +406,14 @@ __device__ inline __attribute__((always_inline)) void pc_bounds(const double* A,
     hi = fmax(Ac + S - P, -Ac + S - N);
 }
 __device__ inline bool nonzero3(const double* A) { return A[0] != 0 || A[1] != 0 || A[2] != 0; }
+// order-preserving 64-bit keys of (non-NaN) doubles, for LDS atomicMax
+__device__ inline unsigned long long okey(double x) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ inline double dkey(unsigned long long k) {
+    return __builtin_bit_cast(double, (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k);
+}
 
 __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
     const int t = blockIdx.x, w = blockIdx.y, tid = threadIdx.x;
@@ -553,6 +561,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
     if (tid == 0) d.pcok[jt] = ok ? 1 : 0;
     if (!ok) return;
     double* const rec = d.pc + jt * 5 * d.pc_cap;
+    uint16_t* const pcp = d.pcp + jt * d.pc_cap;
     const int cap = d.pc_cap;
     for (int pr = tid; pr < NP; pr += blockDim.x) {
         const int l = pr / O, o = pr % O;
@@ -576,6 +585,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
                 rec[2 * cap + q] = A[2];
                 rec[3 * cap + q] = dd + del;
                 rec[4 * cap + q] = -dd + del;
+                pcp[q] = (uint16_t)pr;
                 q++;
             }
     }
@@ -816,73 +826,117 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
                 Gb[nt + ((long)(pr / O) * d.T + t) * O + pr % O] = __builtin_nan("");
             if (tid == 0) atomicAdd(d.cnt + 7, 1u);
         } else if (coll) {
-            // the block's records are staged into LDS (the slicing buffer, free now) in chunks of
-            // PC_CH with coalesced loads; each pair keeps its running maximum across chunks
-            constexpr int PPT = (MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS;
-            constexpr int PC_CH = (MAX_J * CAP_LM * 3 + NF * CAP_UM) / 5;
-            double* const S = ubuf;
+            // Record-parallel scan. Every thread takes records q = tid, tid + 256, ... of the block's
+            // kept planes straight from global memory and forms both candidates, A . c - P before
+            // -A . c - N (position 2 q + neg in the serial scan order). Pass 1: the pair's maximum by
+            // an LDS atomicMax on an order-preserving key; pass 2: the first position holding that
+            // maximum (atomicMin); pass 3: that record publishes its plane. A candidate wins only
+            // above the serial scan's start value (-1e8, strict >), NaN never: the serial scan's
+            // strict-> first maximum, value, plane and sign exactly. The pair tables live in the
+            // slicing buffer (free now).
             const int NP = NJ * O;
             const double* const rec = d.pc + jt * 5 * d.pc_cap;
+            const uint16_t* const pcp = d.pcp + jt * d.pc_cap;
             const int cap = d.pc_cap;
-            const unsigned* const po = d.pcoff + jt * NP;
-            const unsigned last = po[NP - 1];
+            const unsigned last = d.pcoff[jt * NP + NP - 1];
             const int total = (int)(last >> 8) + (int)(last & 255);
-            int q0[PPT], n[PPT];
-            double best[PPT], B[PPT][3];
-            bool isneg[PPT];
-#pragma unroll
-            for (int k = 0; k < PPT; k++) {
-                const int pr = tid + k * EVAL_THREADS;
-                const unsigned v = pr < NP ? po[pr] : 0u;
-                q0[k] = (int)(v >> 8);
-                n[k] = (int)(v & 255);
-                best[k] = -100000000.0;
-                B[k][0] = 0; B[k][1] = 0; B[k][2] = 0;
-                isneg[k] = false;
+            unsigned long long* const pkey = reinterpret_cast<unsigned long long*>(ubuf);  // [NP]
+            unsigned* const pidx = reinterpret_cast<unsigned*>(ubuf + MAX_J * MAX_OBS);      // [NP]
+            double* const pB = ubuf + MAX_J * MAX_OBS + (MAX_J * MAX_OBS + 1) / 2;            // [NP][4]: A, value
+            static_assert(MAX_J * MAX_OBS * 5 + (MAX_J * MAX_OBS + 1) / 2 <= MAX_J * CAP_LM * 3 + NF * CAP_UM, "pair tables");
+            const double start = -100000000.0;
+            for (int pr = tid; pr < NP; pr += blockDim.x) {
+                pkey[pr] = okey(start);
+                pidx[pr] = 0xFFFFFFFFu;
             }
-            for (int r0 = 0; r0 < total; r0 += PC_CH) {
-                const int m = total - r0 < PC_CH ? total - r0 : PC_CH;
-                __syncthreads();
-                for (int i = tid; i < m; i += blockDim.x) {
-                    const double a0 = rec[r0 + i], a1 = rec[cap + r0 + i], a2 = rec[2 * cap + r0 + i];
-                    const double a3 = rec[3 * cap + r0 + i], a4 = rec[4 * cap + r0 + i];
-                    S[i] = a0; S[PC_CH + i] = a1; S[2 * PC_CH + i] = a2; S[3 * PC_CH + i] = a3; S[4 * PC_CH + i] = a4;
+            __syncthreads();
+            auto cand = [&](int q, double& v, int& sub, int& pr, double* a) {
+                a[0] = rec[q];
+                a[1] = rec[cap + q];
+                a[2] = rec[2 * cap + q];
+                const double P = rec[3 * cap + q], N = rec[4 * cap + q];
+                pr = pcp[q];
+                const int l = pr / O;
+                const double Ac = a[0] * lc[l][0] + a[1] * lc[l][1] + a[2] * lc[l][2];
+                const double pos = Ac - P, neg = -Ac - N;
+                sub = (neg > pos || pos != pos) ? 1 : 0;  // the serial scan takes neg only when it beats pos
+                v = sub ? neg : pos;
+            };
+            constexpr int RPT = 3;
+            if (total <= RPT * EVAL_THREADS) {
+                double v[RPT], a[RPT][3];
+                int sub[RPT], pq[RPT];
+#pragma unroll
+                for (int s = 0; s < RPT; s++) {
+                    const int q = tid + s * EVAL_THREADS;
+                    v[s] = start;
+                    sub[s] = 0;
+                    pq[s] = 0;
+                    if (q < total) {
+                        cand(q, v[s], sub[s], pq[s], a[s]);
+                        if (v[s] > start) atomicMax(&pkey[pq[s]], okey(v[s]));
+                    }
                 }
                 __syncthreads();
 #pragma unroll
-                for (int k = 0; k < PPT; k++) {
-                    const int pr = tid + k * EVAL_THREADS;
-                    if (pr >= NP) continue;
-                    const int l = pr / O;
-                    const double c0 = lc[l][0], c1 = lc[l][1], c2 = lc[l][2];
-                    const int lo = (q0[k] > r0 ? q0[k] : r0) - r0, hi = (q0[k] + n[k] < r0 + m ? q0[k] + n[k] : r0 + m) - r0;
-                    for (int q = lo; q < hi; q++) {
-                        const double A0 = S[q], A1 = S[PC_CH + q], A2 = S[2 * PC_CH + q];
-                        const double Ac = A0 * c0 + A1 * c1 + A2 * c2;
-                        const double pos = Ac - S[3 * PC_CH + q];
-                        const double neg = -Ac - S[4 * PC_CH + q];
-                        if (pos > best[k]) { best[k] = pos; B[k][0] = A0; B[k][1] = A1; B[k][2] = A2; isneg[k] = false; }
-                        if (neg > best[k]) { best[k] = neg; B[k][0] = A0; B[k][1] = A1; B[k][2] = A2; isneg[k] = true; }
+                for (int s = 0; s < RPT; s++) {
+                    const int q = tid + s * EVAL_THREADS;
+                    if (q < total && v[s] > start && v[s] == dkey(pkey[pq[s]])) atomicMin(&pidx[pq[s]], (unsigned)(2 * q + sub[s]));
+                }
+                __syncthreads();
+#pragma unroll
+                for (int s = 0; s < RPT; s++) {
+                    const int q = tid + s * EVAL_THREADS;
+                    if (q < total && pidx[pq[s]] == (unsigned)(2 * q + sub[s])) {
+                        double* const b = pB + pq[s] * 4;
+                        b[0] = a[s][0]; b[1] = a[s][1]; b[2] = a[s][2]; b[3] = v[s];
+                    }
+                }
+            } else {
+                for (int q = tid; q < total; q += blockDim.x) {
+                    double v, a[3];
+                    int sub, pr;
+                    cand(q, v, sub, pr, a);
+                    if (v > start) atomicMax(&pkey[pr], okey(v));
+                }
+                __syncthreads();
+                for (int q = tid; q < total; q += blockDim.x) {
+                    double v, a[3];
+                    int sub, pr;
+                    cand(q, v, sub, pr, a);
+                    if (v > start && v == dkey(pkey[pr])) atomicMin(&pidx[pr], (unsigned)(2 * q + sub));
+                }
+                __syncthreads();
+                for (int q = tid; q < total; q += blockDim.x) {
+                    double v, a[3];
+                    int sub, pr;
+                    cand(q, v, sub, pr, a);
+                    if (pidx[pr] == (unsigned)(2 * q + sub)) {
+                        double* const b = pB + pr * 4;
+                        b[0] = a[0]; b[1] = a[1]; b[2] = a[2]; b[3] = v;
                     }
                 }
             }
-#pragma unroll
-            for (int k = 0; k < PPT; k++) {
-                const int pr = tid + k * EVAL_THREADS;
-                if (pr >= NP) continue;
+            __syncthreads();
+            for (int pr = tid; pr < NP; pr += blockDim.x) {
                 const int l = pr / O, o = pr % O;
+                const unsigned wi = pidx[pr];
+                const bool won = wi != 0xFFFFFFFFu, isneg = won && (wi & 1u);
+                const double* const b = pB + pr * 4;
+                const double best = won ? b[3] : start;
+                const double B0 = won ? b[0] : 0.0, B1 = won ? b[1] : 0.0, B2 = won ? b[2] : 0.0;
                 const long row = nt + ((long)l * d.T + t) * O + o;
-                Gb[row] = -best[k];
+                Gb[row] = -best;
                 // J = isneg ? B . dc : -(B . dc) = n . dc with n = isneg ? B : -B (negation is exact)
                 double* const jn = Jnb + (row - nt) * 3;
-                jn[0] = isneg[k] ? B[k][0] : -B[k][0];
-                jn[1] = isneg[k] ? B[k][1] : -B[k][1];
-                jn[2] = isneg[k] ? B[k][2] : -B[k][2];
+                jn[0] = isneg ? B0 : -B0;
+                jn[1] = isneg ? B1 : -B1;
+                jn[2] = isneg ? B2 : -B2;
                 if (mode == 0) {
 #pragma unroll
                     for (int kk = 0; kk < NF; kk++) {
-                        const double dot = B[k][0] * dlc[l][kk][0] + B[k][1] * dlc[l][kk][1] + B[k][2] * dlc[l][kk][2];
-                        Jb[row * NF + kk] = isneg[k] ? dot : -dot;
+                        const double dot = B0 * dlc[l][kk][0] + B1 * dlc[l][kk][1] + B2 * dlc[l][kk][2];
+                        Jb[row * NF + kk] = isneg ? dot : -dot;
                     }
                 }
             }
@@ -1037,12 +1091,9 @@ template __global__ void eval_kernel_t<double, true, true>(NlpDev, int);
 // remaining trial points of world wl[i] (alpha halved k times from the round's alpha: the points
 // ipm_world_C's sequential rounds would visit) — the constraint values and the cost, all the
 // acceptance test reads (ipm_rows_Cs / ipm_world_Cs); the Jacobian is formed only for the trial
-// chosen, by a full evaluation (eval_kernel_t mode 5). The monomials and the certified-plane
-// records are staged once for all K points; every value is formed with eval_kernel_t's arithmetic.
-// IPT: (trial, pair) items per thread, >= ceil(K * NJ * O / EVAL_THREADS) (planner.hip picks the
-// smallest instantiation: 6 covers K = 9 trials of up to 170 pairs, e.g. 7 links x 20 obstacles;
-// 10 up to 284, e.g. 7 x 40)
-template <int IPT>
+// chosen, by a full evaluation (eval_kernel_t mode 5). The monomials are staged and each
+// certified-plane record is loaded once for all K points; every value is formed with
+// eval_kernel_t's arithmetic.
 __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
     const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
     const WorldState& S = d.ws[w];
@@ -1180,64 +1231,39 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
         d.fs[(long)i * K + kk] = fv * rp.cost_scale;
     }
     __syncthreads();
-    // collision rows of every trial from the plane cache: one item per (trial, pair) scans the pair's
-    // kept planes in order (first maximum, strict >); the records staged in LDS chunks, each item's
-    // running maximum kept across chunks
-    constexpr int PC_CH = (MAX_J * CAP_LM * 3 + NF * CAP_UM) / 5;
-    double* const Sr = ubuf;
+    // collision rows of every trial from the plane cache, record-parallel as eval_kernel_t's scan:
+    // every thread takes records straight from global memory and forms each trial's two candidates;
+    // the (trial, pair) maximum by an LDS atomicMax on an order-preserving key (the value is all a
+    // trial needs; a +-0 tie cannot change the line search's terms). Tables in the slicing buffer.
     const double* const rec = d.pc + jt * 5 * d.pc_cap;
+    const uint16_t* const pcp = d.pcp + jt * d.pc_cap;
     const int cap = d.pc_cap;
-    const unsigned* const po = d.pcoff + jt * NP;
-    const unsigned last = NP > 0 ? po[NP - 1] : 0u;
+    const unsigned last = NP > 0 ? d.pcoff[jt * NP + NP - 1] : 0u;
     const int total = (int)(last >> 8) + (int)(last & 255);
-    const int nitem = K * NP;
-    int q0[IPT], n[IPT];
-    double best[IPT], c0[IPT], c1[IPT], c2[IPT];
-#pragma unroll
-    for (int s = 0; s < IPT; s++) {
-        const int u = tid + s * EVAL_THREADS;
-        const int kk = u / (NP > 0 ? NP : 1), pr = u - kk * NP;
-        const unsigned v = u < nitem ? po[pr] : 0u;
-        q0[s] = (int)(v >> 8);
-        n[s] = (int)(v & 255);
-        best[s] = -100000000.0;
-        const int l = u < nitem ? pr / O : 0, kc = u < nitem ? kk : 0;
-        c0[s] = lck[kc][l][0]; c1[s] = lck[kc][l][1]; c2[s] = lck[kc][l][2];
-    }
-    for (int r0 = 0; r0 < total; r0 += PC_CH) {
-        const int m = total - r0 < PC_CH ? total - r0 : PC_CH;
-        __syncthreads();
-        for (int u = tid; u < m; u += blockDim.x) {
-            const double a0 = rec[r0 + u], a1 = rec[cap + r0 + u], a2 = rec[2 * cap + r0 + u];
-            const double a3 = rec[3 * cap + r0 + u], a4 = rec[4 * cap + r0 + u];
-            Sr[u] = a0; Sr[PC_CH + u] = a1; Sr[2 * PC_CH + u] = a2; Sr[3 * PC_CH + u] = a3; Sr[4 * PC_CH + u] = a4;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int s = 0; s < IPT; s++) {
-            const int lo = (q0[s] > r0 ? q0[s] : r0) - r0, hi = (q0[s] + n[s] < r0 + m ? q0[s] + n[s] : r0 + m) - r0;
-            for (int q = lo; q < hi; q++) {
-                const double Ac = Sr[q] * c0[s] + Sr[PC_CH + q] * c1[s] + Sr[2 * PC_CH + q] * c2[s];
-                const double pos = Ac - Sr[3 * PC_CH + q];
-                const double neg = -Ac - Sr[4 * PC_CH + q];
-                if (pos > best[s]) best[s] = pos;
-                if (neg > best[s]) best[s] = neg;
-            }
+    unsigned long long* const pkey = reinterpret_cast<unsigned long long*>(ubuf);  // [K][NP]
+    static_assert(EV_MAXK * MAX_J * MAX_OBS <= MAX_J * CAP_LM * 3 + NF * CAP_UM, "trial pair table");
+    const double start = -100000000.0;
+    for (int u = tid; u < K * NP; u += blockDim.x) pkey[u] = okey(start);
+    __syncthreads();
+    for (int q = tid; q < total; q += blockDim.x) {
+        const double a0 = rec[q], a1 = rec[cap + q], a2 = rec[2 * cap + q];
+        const double P = rec[3 * cap + q], N = rec[4 * cap + q];
+        const int pr = pcp[q], l = pr / O;
+        for (int kk = 0; kk < K; kk++) {
+            const double Ac = a0 * lck[kk][l][0] + a1 * lck[kk][l][1] + a2 * lck[kk][l][2];
+            const double pos = Ac - P, neg = -Ac - N;
+            const double v = (neg > pos || pos != pos) ? neg : pos;
+            if (v > start) atomicMax(&pkey[kk * NP + pr], okey(v));
         }
     }
-#pragma unroll
-    for (int s = 0; s < IPT; s++) {
-        const int u = tid + s * EVAL_THREADS;
-        if (u >= nitem) continue;
+    __syncthreads();
+    for (int u = tid; u < K * NP; u += blockDim.x) {
         const int kk = u / NP, pr = u - kk * NP;
         const int l = pr / O, o = pr % O;
-        d.gs[((long)i * K + kk) * d.m + nt + ((long)l * d.T + t) * O + o] = -best[s];
+        d.gs[((long)i * K + kk) * d.m + nt + ((long)l * d.T + t) * O + o] = -dkey(pkey[u]);
     }
 }
 
-template __global__ void eval_trials_kernel<6>(NlpDev);
-template __global__ void eval_trials_kernel<10>(NlpDev);
-template __global__ void eval_trials_kernel<(EV_MAXK * MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS>(NlpDev);
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM

@@ -368,7 +368,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
     d.pcready = 0;
     d.pc_cap = PC_K * NJ * Om;
-    if (d.pcache && ((rc = p->alloc(&d.pc, jobs * 5 * (size_t)d.pc_cap)) || (rc = p->alloc(&d.pcoff, jobs * NJ * (size_t)Om)) ||
+    if (d.pcache && ((rc = p->alloc(&d.pc, jobs * 5 * (size_t)d.pc_cap)) || (rc = p->alloc(&d.pcp, jobs * (size_t)d.pc_cap)) ||
+                     (rc = p->alloc(&d.pcoff, jobs * NJ * (size_t)Om)) ||
                      (rc = p->alloc(&d.pcok, jobs))))
         return rc;
     // speculative line-search slots (values only): every world x (max_ls - 1) trials. The speculative
@@ -647,11 +648,7 @@ static int run_solver(armour_planner* p) {
             // tests in trial order, then the chosen trial in full
             NlpDev ds = d;
             ds.wl = Ls[1];
-            constexpr int IPT_MAX = (EV_MAXK * MAX_J * MAX_OBS + EVAL_THREADS - 1) / EVAL_THREADS;
-            const int items = d.K * p->NJ * d.O;
-            auto tk = items <= 6 * EVAL_THREADS ? eval_trials_kernel<6>
-                      : items <= 10 * EVAL_THREADS ? eval_trials_kernel<10> : eval_trials_kernel<IPT_MAX>;
-            hipLaunchKernelGGL(tk, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(eval_trials_kernel, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nsearch * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nsearch), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nsearch), ds, 5);
