@@ -34,6 +34,7 @@ struct LaneArgs {
     unsigned long long* bytes;
     double* dump;          // optional [nops][DUMP_W][LG] of bundle 0 (null: off)
     unsigned long long* prof;  // optional [2 * nops + 16] per-op cycles/terms + phase cycles
+    unsigned long long* btime; // optional [bundles][2]: start / end wall clock of every bundle
     unsigned long long* occ;   // [8] largest use over the launch: arena hashes, arena rows, operator
                                // terms, link / torque k-only monomials (capacity headroom)
     const int* wlist;      // null: every world of the batch; else only these worlds (a retry)
@@ -112,8 +113,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
         x.job = a.wlist ? (long)a.wlist[job / a.T] * a.T + job % a.T : job;
         x.jrs = a.jrs + x.job * NF;
         __syncthreads();
+        const unsigned long long t0 = a.btime ? wall_clock64() : 0;
         run_program(x, rp, a.prog, a.nops, out, b == 0 ? a.dump : nullptr);
         __syncthreads();
+        if (a.btime && x.tid == 0) {
+            a.btime[2 * b] = t0;
+            a.btime[2 * b + 1] = wall_clock64();
+        }
         if (err && x.wave == 0 && x.valid) atomicOr(&out.err[x.job / a.T], err);
         if (x.tid == 0) {
             atomicAdd(a.bytes, arena.bytes);

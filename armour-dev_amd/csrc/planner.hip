@@ -80,6 +80,7 @@ struct armour_planner {
     bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
     int lane_grid = 0;
     lane::LaneArgs la;
+
     // nlp
     NlpDev d;
     int* feas = nullptr;
@@ -217,8 +218,12 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         HIPCK(hipMemcpy(p->d_prog, pb.ops.data(), sizeof(Op) * pb.ops.size(), hipMemcpyHostToDevice));
         HIPCK(hipMemcpy(p->d_slot_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
         if (std::getenv("ARMOUR_PROFILE_OPS")) {
-            if ((rc = p->alloc(&p->d_prof, 2 * pb.ops.size() + 16 + 8 * OP_NCODES))) return rc;
-            HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * (2 * pb.ops.size() + 16 + 8 * OP_NCODES)));
+            // =3: no op profiling; [start, end] wall clock (100 MHz) of every bundle of the last launch
+            // after the op tables (bundle-engine load balance)
+            const size_t nbt = 2 * (((size_t)p->Wmax * p->T + lane::LG - 1) / lane::LG);
+            const size_t n = 2 * pb.ops.size() + 16 + 8 * OP_NCODES + nbt;
+            if ((rc = p->alloc(&p->d_prof, n))) return rc;
+            HIPCK(hipMemset(p->d_prof, 0, sizeof(unsigned long long) * n));
         }
     }
     // reach workspace: four resident workgroups per CU, each with a private arena
@@ -312,7 +317,9 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         la.slot_off = p->d_slot_off;
         la.nslots = p->nslots;
         la.bytes = p->d_bytes;
-        la.prof = p->d_prof;
+        const bool btimes = pm && std::atoi(pm) == 3;
+        la.prof = btimes ? nullptr : p->d_prof;
+        la.btime = btimes ? p->d_prof + 2 * p->nops + 16 + 8 * OP_NCODES : nullptr;
         la.dump = nullptr;
         if (p->d_dump) {
             (void)hipFree(p->d_dump);
@@ -1013,8 +1020,12 @@ int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms
     if (!p->d_prof) return fail(ARMOUR_E_STATE, "op profiling is off (set ARMOUR_PROFILE_OPS before armour_create)");
     // capacity in pairs: nops + 8 -> per-op [cycles, terms] + 16 phase totals; nops + 8 + 4 * OP_NCODES
     // adds the bundle engine's phase cycles per op code [OP_NCODES][8]
+    // adds the bundle engine's phase cycles per op code [OP_NCODES][8]; + ceil(max_worlds * T / 64)
+    // adds every bundle's [start, end] wall clock (ARMOUR_PROFILE_OPS=3)
     if (cycles_terms && capacity >= p->nops + 8) {
-        const size_t n = capacity >= p->nops + 8 + 4 * OP_NCODES ? 2 * p->nops + 16 + 8 * OP_NCODES : 2 * p->nops + 16;
+        const size_t nb = ((size_t)p->Wmax * p->T + lane::LG - 1) / lane::LG;
+        const size_t n = capacity >= p->nops + 8 + 4 * OP_NCODES + (long)nb ? 2 * p->nops + 16 + 8 * OP_NCODES + 2 * nb
+                         : capacity >= p->nops + 8 + 4 * OP_NCODES ? 2 * p->nops + 16 + 8 * OP_NCODES : 2 * p->nops + 16;
         HIPCK(hipMemcpy(cycles_terms, p->d_prof, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
     }
     return p->nops;
