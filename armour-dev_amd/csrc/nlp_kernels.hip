@@ -1575,8 +1575,10 @@ __device__ inline void world_A_body(const NlpDev& d, int w, int nside) {
     }
 }
 
-// pass B: step components, fraction to boundary, line-search ingredients
-__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_B(NlpDev d) {
+// pass B: step components, fraction to boundary, line-search ingredients. Held to four waves per
+// SIMD (128 VGPRs, 2 spilled): 3.66 ms per 327-world solve against 3.95 at three. ipm_rows_DA held
+// to three spills 32 registers and slows from 6.5 to 7.9 ms, so it stays at two.
+__global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void ipm_rows_B(NlpDev d) {
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
