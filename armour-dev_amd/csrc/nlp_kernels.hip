@@ -428,6 +428,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
     __shared__ unsigned char mixbits[MAX_J * MAX_OBS * OBS_GEN];
     __shared__ double pairM[MAX_J * MAX_OBS];
     __shared__ unsigned cntp[MAX_J * MAX_OBS];
+    __shared__ unsigned long long pbits[MAX_J * MAX_OBS];  // surviving planes of a pair, bit = scan position
     __shared__ unsigned total_s;
     for (int i = tid; i < NJ * 18; i += blockDim.x) lgen[i / 18][i % 18] = d.ro.link_gens[jt * NJ * 18 + i];
     for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
@@ -532,9 +533,16 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
         double G[BUF_GEN][3], oc[3];
         load_gens(l, o, G, oc);
         unsigned n = 0;
+        unsigned long long bits = 0;
+        int pos = 0;
         for (int a = 0; a < BUF_GEN; a++)
-            for (int b = a + 1; b < BUF_GEN; b++) n += survives(pr, l, o, a, b, G, oc) ? 1 : 0;
+            for (int b = a + 1; b < BUF_GEN; b++, pos++)
+                if (survives(pr, l, o, a, b, G, oc)) {
+                    n++;
+                    bits |= 1ull << pos;
+                }
         cntp[pr] = n;
+        pbits[pr] = bits;
     }
     __syncthreads();
     if (tid < 64) {  // exclusive prefix over the pairs, one wave: lane k sums a contiguous chunk
@@ -568,9 +576,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
         double G[BUF_GEN][3], oc[3];
         load_gens(l, o, G, oc);
         unsigned q = cntp[pr];
+        const unsigned long long bits = pbits[pr];
+        int pos = 0;
         for (int a = 0; a < BUF_GEN; a++)
             for (int b = a + 1; b < BUF_GEN; b++) {
-                if (!survives(pr, l, o, a, b, G, oc)) continue;
+                if (!((bits >> pos++) & 1ull)) continue;
                 double A[3], dd, del;
                 if (a < OBS_GEN && b >= OBS_GEN) {
                     mixed_plane_j(b - OBS_GEN, G[a], G, oc, A, dd, del);
@@ -1783,15 +1793,13 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
     __shared__ double lds[(ROW_THREADS / 64) * 53];
-    double alpha = S.alpha, xt[NF];
+    double alpha = S.alpha;
     for (int q = 0; q < k; q++) alpha *= 0.5;
-#pragma unroll
-    for (int j = 0; j < NF; j++) xt[j] = S.x[j] + alpha * S.dx[j];
     const double* G = d.gs + (long)blockIdx.y * d.m;
     double logt = 0, rpt = 0;
     const long r0 = (long)blockIdx.x * d.chunk;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
-        const double v = r < d.m ? G[r] : xt[r - d.m];
+        const double v = r < d.m ? G[r] : S.x[r - d.m] + alpha * S.dx[r - d.m];  // box row: the trial's x
         const long ii = (long)w * d.R + r;
         double L, U;
         row_bounds(d, ii, (int)r, L, U);
