@@ -609,9 +609,18 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
 // ARMTD selects the comparison planner's extrema and cost at compile time: a call into them from
 // the ARMOUR instantiation would cost it registers and a stack frame (occupancy 4 -> 3 waves/SIMD)
 // CACHED (fp64 only): the collision rows from the certified plane cache, for points in its box
-// (every solver point; armour_eval_constraints checks x on the host); otherwise the full scan
-template <typename R, bool ARMTD, bool CACHED>
-__global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
+// (every solver point; armour_eval_constraints checks x on the host); otherwise the full scan.
+// LM, UM, UB: LDS capacities — monomials per link / torque PZ and the staging buffer (doubles).
+// eval_kernel_t reserves the reach's caps (CAP_LM, CAP_UM); eval_kernel_small the small ones, for
+// batches whose largest PZs and pair tables fit (planner.hip checks), at a third of the LDS and five
+// resident blocks per CU instead of four.
+constexpr int UB_FULL = MAX_J * CAP_LM * 3 + NF * CAP_UM;
+constexpr int LM_S = 16, UM_S = 64;
+constexpr int UB_S = 1544;   // >= MAX_J * LM_S * 3 + NF * UM_S, and the pair tables of 280 pairs (5.5 NP + 1)
+static_assert(UB_S >= MAX_J * LM_S * 3 + NF * UM_S, "small staging buffer");
+__host__ __device__ constexpr int eval_pair_doubles(int np) { return np + (np + 1) / 2 + 4 * np; }
+template <typename R, bool ARMTD, bool CACHED, int LM, int UM, int UB>
+__device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mode) {
     static_assert(!CACHED || std::is_same<R, double>::value, "the plane cache is fp64");
     // mode 5: the trial point the speculative round chose (ipm_world_Cs: spec_k >= 0), in full,
     // into the world's trial slot (list entries, blockIdx.y -> wl)
@@ -640,16 +649,17 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
     __shared__ R dlc[MAX_J][NF][3];
     __shared__ R lgen[MAX_J][18];
     __shared__ R obs[MAX_OBS][12];
-    __shared__ uint16_t lh[MAX_J][CAP_LM];
-    __shared__ uint16_t th[NF][CAP_UM];
+    __shared__ uint16_t lh[MAX_J][LM];
+    __shared__ uint16_t th[NF][UM];
     // monomial coefficients while slicing; afterwards the same LDS holds the obstacle-independent
-    // link-link planes and the link-independent obstacle-obstacle planes
-    __shared__ double ubuf[MAX_J * CAP_LM * 3 + NF * CAP_UM];
-    auto lco = reinterpret_cast<R (*)[CAP_LM][3]>(ubuf);
-    auto tco = reinterpret_cast<R (*)[CAP_UM]>(ubuf + MAX_J * CAP_LM * 3);
+    // link-link planes and the link-independent obstacle-obstacle planes (full scan), or the pair
+    // tables of the cached scan
+    __shared__ double ubuf[UB];
+    static_assert(MAX_J * LM * 3 + NF * UM <= UB, "monomial staging");
+    auto lco = reinterpret_cast<R (*)[LM][3]>(ubuf);
+    auto tco = reinterpret_cast<R (*)[UM]>(ubuf + MAX_J * LM * 3);
     constexpr int NMIX = MAX_J * MAX_OBS * OBS_GEN;
-    static_assert(MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5 + NMIX + (NMIX + 7) / 8 <= MAX_J * CAP_LM * 3 + NF * CAP_UM,
-                  "plane tables");
+    static_assert(CACHED || MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5 + NMIX + (NMIX + 7) / 8 <= UB, "plane tables");
     auto llp = reinterpret_cast<R (*)[LL_PLANES][10]>(ubuf);
     auto oop = reinterpret_cast<R (*)[OO_PLANES][5]>(ubuf + MAX_J * LL_PLANES * 10);
     R* mixv = reinterpret_cast<R*>(ubuf + MAX_J * LL_PLANES * 10 + MAX_OBS * OO_PLANES * 5);   // per (link, obstacle, i)
@@ -850,10 +860,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
             const int cap = d.pc_cap;
             const unsigned last = d.pcoff[jt * NP + NP - 1];
             const int total = (int)(last >> 8) + (int)(last & 255);
+            // eval_pair_doubles(NP) <= UB: always for UB_FULL, checked by the host for UB_S
             unsigned long long* const pkey = reinterpret_cast<unsigned long long*>(ubuf);  // [NP]
-            unsigned* const pidx = reinterpret_cast<unsigned*>(ubuf + MAX_J * MAX_OBS);      // [NP]
-            double* const pB = ubuf + MAX_J * MAX_OBS + (MAX_J * MAX_OBS + 1) / 2;            // [NP][4]: A, value
-            static_assert(MAX_J * MAX_OBS * 5 + (MAX_J * MAX_OBS + 1) / 2 <= MAX_J * CAP_LM * 3 + NF * CAP_UM, "pair tables");
+            unsigned* const pidx = reinterpret_cast<unsigned*>(ubuf + NP);                   // [NP]
+            double* const pB = ubuf + NP + (NP + 1) / 2;                                     // [NP][4]: A, value
+            static_assert(eval_pair_doubles(MAX_J * MAX_OBS) <= UB_FULL, "pair tables");
             const double start = -100000000.0;
             for (int pr = tid; pr < NP; pr += blockDim.x) {
                 pkey[pr] = okey(start);
@@ -1089,6 +1100,13 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode
 // the product evaluation is fp64; eval_kernel_t<float> serves only the fp32 tolerance study
 // (ARMOUR_EVAL_F32, tools/fp32_study.py): reach sets stay fp64, the slicing and collision
 // arithmetic runs in float
+template <typename R, bool ARMTD, bool CACHED>
+__global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
+    eval_body<R, ARMTD, CACHED, CAP_LM, CAP_UM, UB_FULL>(d, mode);
+}
+__global__ __launch_bounds__(EVAL_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void eval_kernel_small(NlpDev d, int mode) {
+    eval_body<double, false, true, LM_S, UM_S, UB_S>(d, mode);
+}
 template __global__ void eval_kernel_t<double, false, false>(NlpDev, int);
 template __global__ void eval_kernel_t<float, false, false>(NlpDev, int);
 template __global__ void eval_kernel_t<double, true, false>(NlpDev, int);
@@ -1104,7 +1122,11 @@ template __global__ void eval_kernel_t<double, true, true>(NlpDev, int);
 // chosen, by a full evaluation (eval_kernel_t mode 5). The monomials are staged and each
 // certified-plane record is loaded once for all K points; every value is formed with
 // eval_kernel_t's arithmetic.
-__global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
+// LM, UM, UB as eval_body; the staging buffer then holds the (trial, pair) keys, K * NP <= UB
+constexpr int UB_TS = EV_MAXK * 280;   // small variant: 9 trials of up to 280 pairs (7 links x 40 obstacles)
+static_assert(UB_TS >= MAX_J * LM_S * 3 + NF * UM_S, "small trials staging buffer");
+template <int LM, int UM, int UB>
+__device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d) {
     const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
@@ -1116,12 +1138,13 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
     __shared__ double xk[EV_MAXK][NF];
     __shared__ double ptab[EV_MAXK][NF][4];  // x_j^g of trial k (the value slices' factors)
     __shared__ double lck[EV_MAXK][MAX_J][3];
-    __shared__ uint16_t lh[MAX_J][CAP_LM];
-    __shared__ uint16_t th[NF][CAP_UM];
-    __shared__ double ubuf[MAX_J * CAP_LM * 3 + NF * CAP_UM];
+    __shared__ uint16_t lh[MAX_J][LM];
+    __shared__ uint16_t th[NF][UM];
+    __shared__ double ubuf[UB];
+    static_assert(MAX_J * LM * 3 + NF * UM <= UB, "monomial staging");
     __shared__ int lcnt[MAX_J], tcnt[NF];
-    auto lco = reinterpret_cast<double (*)[CAP_LM][3]>(ubuf);
-    auto tco = reinterpret_cast<double (*)[CAP_UM]>(ubuf + MAX_J * CAP_LM * 3);
+    auto lco = reinterpret_cast<double (*)[LM][3]>(ubuf);
+    auto tco = reinterpret_cast<double (*)[UM]>(ubuf + MAX_J * LM * 3);
     if (tid < K * NF) {
         const int kk = tid / NF, j = tid % NF;
         double a = S.alpha;
@@ -1251,7 +1274,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
     const unsigned last = NP > 0 ? d.pcoff[jt * NP + NP - 1] : 0u;
     const int total = (int)(last >> 8) + (int)(last & 255);
     unsigned long long* const pkey = reinterpret_cast<unsigned long long*>(ubuf);  // [K][NP]
-    static_assert(EV_MAXK * MAX_J * MAX_OBS <= MAX_J * CAP_LM * 3 + NF * CAP_UM, "trial pair table");
+    static_assert(EV_MAXK * MAX_J * MAX_OBS <= UB_FULL, "trial pair table");  // K * NP <= UB_TS: host check
     const double start = -100000000.0;
     for (int u = tid; u < K * NP; u += blockDim.x) pkey[u] = okey(start);
     __syncthreads();
@@ -1273,7 +1296,37 @@ __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) {
         d.gs[((long)i * K + kk) * d.m + nt + ((long)l * d.T + t) * O + o] = -dkey(pkey[u]);
     }
 }
+__global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) { eval_trials_body<CAP_LM, CAP_UM, UB_FULL>(d); }
+__global__ __launch_bounds__(EVAL_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void eval_trials_small(NlpDev d) {
+    eval_trials_body<LM_S, UM_S, UB_TS>(d);
+}
 
+// the largest link / torque k-monomial counts of a reach (nt = 0: no torque PZs): block b writes
+// the maxima of its grid-stride slice to out[2 b], out[2 b + 1]; the host takes the max over blocks
+// and picks the evaluation kernels' LDS capacities from them
+constexpr int MONO_BLOCKS = 64;
+__global__ __launch_bounds__(256) void mono_max_kernel(ReachOut ro, long nl, long nt, int* out) {
+    int ml = 0, mt = 0;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) ml = max(ml, ro.link_cnt[i]);
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += stride) mt = max(mt, ro.tq_cnt[i]);
+    __shared__ int r[2][4];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        ml = max(ml, __shfl_xor(ml, off));
+        mt = max(mt, __shfl_xor(mt, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        r[0][threadIdx.x >> 6] = ml;
+        r[1][threadIdx.x >> 6] = mt;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        int m = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); k++) m = max(m, r[threadIdx.x][k]);
+        out[2 * blockIdx.x + threadIdx.x] = m;
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // armour-IPM

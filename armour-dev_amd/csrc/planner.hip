@@ -78,6 +78,10 @@ struct armour_planner {
     long job_max = 0;         // batches of at most this many jobs (W x T) run on the per-job engine
     bool job_fits = true;     // the reach program's payload pool fits the per-job engine's LDS
     bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
+    bool eval_full = false;   // ARMOUR_EVAL_FULL: always the full-capacity evaluation kernels
+    int* d_mono_max = nullptr;  // [MONO_BLOCKS][2] per-block largest link / torque k-monomial counts
+    int h_mono[2 * MONO_BLOCKS] = {};
+    int mono_max[2] = {CAP_LM, CAP_UM};  // of the last reach
     int lane_grid = 0;
     lane::LaneArgs la;
 
@@ -265,10 +269,12 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         HIPCK(hipMemset(p->d_dump, 0, sizeof(double) * p->nops * DUMP_W));
         ra.dump = p->d_dump;
     }
-    if ((rc = p->alloc(&p->d_jrs, jobs * NF))) return rc;
+    if ((rc = p->alloc(&p->d_jrs, jobs * NF)) || (rc = p->alloc(&p->d_mono_max, 2 * MONO_BLOCKS))) return rc;
     {
         const char* f32 = std::getenv("ARMOUR_EVAL_F32");
         p->eval_f32 = f32 && std::atoi(f32) != 0;
+        const char* ef = std::getenv("ARMOUR_EVAL_FULL");
+        p->eval_full = ef && std::atoi(ef) != 0;
     }
     if (p->has_job) {
         ra.arena_cap = 1 << 17;
@@ -510,6 +516,9 @@ static int run_reach(armour_planner* p) {
     HIPCK(hipEventRecord(p->ev[4], rs));
     std::vector<int> err(p->W);
     unsigned long long bytes = 0;
+    hipLaunchKernelGGL(mono_max_kernel, dim3(MONO_BLOCKS), dim3(256), 0, rs, p->ro, jobs * p->NJ, p->armtd ? 0 : jobs * (long)NF,
+                       p->d_mono_max);
+    HIPCK(hipMemcpyAsync(p->h_mono, p->d_mono_max, sizeof(p->h_mono), hipMemcpyDeviceToHost, rs));
     HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
     HIPCK(hipMemcpyAsync(&bytes, p->d_bytes, sizeof(bytes), hipMemcpyDeviceToHost, rs));
     HIPCK(hipStreamSynchronize(rs));
@@ -546,8 +555,16 @@ static int run_reach(armour_planner* p) {
         hipLaunchKernelGGL(lane::lane_reach_kernel, dim3((int)(bundles < g ? bundles : g)), dim3(lane::LT), 0, rs,
                            p->d_rp, la, p->ro);
         HIPCK(hipGetLastError());
+        hipLaunchKernelGGL(mono_max_kernel, dim3(MONO_BLOCKS), dim3(256), 0, rs, p->ro, jobs * p->NJ,
+                           p->armtd ? 0 : jobs * (long)NF, p->d_mono_max);
+        HIPCK(hipMemcpyAsync(p->h_mono, p->d_mono_max, sizeof(p->h_mono), hipMemcpyDeviceToHost, rs));
         HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
         HIPCK(hipStreamSynchronize(rs));
+    }
+    p->mono_max[0] = p->mono_max[1] = 0;
+    for (int b = 0; b < MONO_BLOCKS; b++) {
+        p->mono_max[0] = std::max(p->mono_max[0], p->h_mono[2 * b]);
+        p->mono_max[1] = std::max(p->mono_max[1], p->h_mono[2 * b + 1]);
     }
     // constraint bounds from the (final) torque radii
     const long rows = (long)p->W * d.R;
@@ -588,8 +605,17 @@ static int nside_count(const armour_planner* p) {
 // (the ARMTD planner's extrema and cost in their own instantiation)
 // and the collision rows from the certified plane cache when it is built (points in its box: every
 // solver point; `cached` = false for a caller's x outside it)
+// the small-capacity evaluation kernels (eval_kernel_small, eval_trials_small: a third of the LDS,
+// five blocks per CU) when the last reach's largest PZs and this batch's pair tables fit them
+static bool eval_small_fits(const armour_planner* p) {
+    return !p->eval_full && !p->armtd && !p->eval_f32 && p->mono_max[0] <= LM_S && p->mono_max[1] <= UM_S;
+}
 static void launch_eval(armour_planner* p, dim3 grid, const NlpDev& d, int mode, bool cached = true) {
     const bool c = cached && d.pcready && d.O > 0;
+    if (c && eval_small_fits(p) && eval_pair_doubles(p->NJ * d.O) <= UB_S) {
+        hipLaunchKernelGGL(eval_kernel_small, grid, dim3(EVAL_THREADS), 0, p->stream, d, mode);
+        return;
+    }
     auto k = p->eval_f32 ? (d.armtd ? eval_kernel_t<float, true, false> : eval_kernel_t<float, false, false>)
                          : c ? (d.armtd ? eval_kernel_t<double, true, true> : eval_kernel_t<double, false, true>)
                              : (d.armtd ? eval_kernel_t<double, true, false> : eval_kernel_t<double, false, false>);
@@ -655,7 +681,10 @@ static int run_solver(armour_planner* p) {
             // tests in trial order, then the chosen trial in full
             NlpDev ds = d;
             ds.wl = Ls[1];
-            hipLaunchKernelGGL(eval_trials_kernel, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, ds);
+            if (eval_small_fits(p) && d.K * p->NJ * d.O <= UB_TS)
+                hipLaunchKernelGGL(eval_trials_small, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, ds);
+            else
+                hipLaunchKernelGGL(eval_trials_kernel, dim3(p->T, nsearch), dim3(EVAL_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nsearch * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nsearch), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nsearch), ds, 5);
