@@ -612,8 +612,10 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
 // (every solver point; armour_eval_constraints checks x on the host); otherwise the full scan.
 // LM, UM, UB: LDS capacities — monomials per link / torque PZ and the staging buffer (doubles).
 // eval_kernel_t reserves the reach's caps (CAP_LM, CAP_UM); eval_kernel_small the small ones, for
-// batches whose largest PZs and pair tables fit (planner.hip checks), at a third of the LDS and five
-// resident blocks per CU instead of four.
+// batches whose largest PZs and pair tables fit (planner.hip checks): 16 KB of LDS, held to eight
+// waves per SIMD (64 VGPRs, 26 spilled) — eight resident blocks per CU instead of four. Measured per
+// 327-world solve: 16.4 ms (four blocks), 16.1 (five), 14.9 (six), 14.1 (seven), 13.6 (eight); the
+// latency of the staged phases hides behind more blocks, the spills cost less.
 constexpr int UB_FULL = MAX_J * CAP_LM * 3 + NF * CAP_UM;
 constexpr int LM_S = 16, UM_S = 64;
 constexpr int UB_S = 1544;   // >= MAX_J * LM_S * 3 + NF * UM_S, and the pair tables of 280 pairs (5.5 NP + 1)
@@ -1104,7 +1106,7 @@ template <typename R, bool ARMTD, bool CACHED>
 __global__ __launch_bounds__(EVAL_THREADS) void eval_kernel_t(NlpDev d, int mode) {
     eval_body<R, ARMTD, CACHED, CAP_LM, CAP_UM, UB_FULL>(d, mode);
 }
-__global__ __launch_bounds__(EVAL_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void eval_kernel_small(NlpDev d, int mode) {
+__global__ __launch_bounds__(EVAL_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8))) void eval_kernel_small(NlpDev d, int mode) {
     eval_body<double, false, true, LM_S, UM_S, UB_S>(d, mode);
 }
 template __global__ void eval_kernel_t<double, false, false>(NlpDev, int);
@@ -1297,6 +1299,7 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     }
 }
 __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) { eval_trials_body<CAP_LM, CAP_UM, UB_FULL>(d); }
+// five waves per SIMD (91 VGPRs): six measured slower (5.5 -> 5.7 ms per solve)
 __global__ __launch_bounds__(EVAL_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void eval_trials_small(NlpDev d) {
     eval_trials_body<LM_S, UM_S, UB_TS>(d);
 }
