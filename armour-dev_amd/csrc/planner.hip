@@ -79,9 +79,13 @@ struct armour_planner {
     bool job_fits = true;     // the reach program's payload pool fits the per-job engine's LDS
     bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
     bool eval_full = false;   // ARMOUR_EVAL_FULL: always the full-capacity evaluation kernels
-    int* d_mono_max = nullptr;  // [MONO_BLOCKS][2] per-block largest link / torque k-monomial counts
+    // largest link / torque k-monomial counts of the last reach: the bundle engine records them
+    // (d_occ[3], d_occ[4], copied with the error flags); the per-job engine's batches take
+    // mono_max_kernel's per-block maxima [MONO_BLOCKS][2]
+    int* d_mono_max = nullptr;
     int h_mono[2 * MONO_BLOCKS] = {};
-    int mono_max[2] = {CAP_LM, CAP_UM};  // of the last reach
+    unsigned long long h_occ[8] = {};
+    int mono_max[2] = {CAP_LM, CAP_UM};
     int lane_grid = 0;
     lane::LaneArgs la;
 
@@ -516,9 +520,15 @@ static int run_reach(armour_planner* p) {
     HIPCK(hipEventRecord(p->ev[4], rs));
     std::vector<int> err(p->W);
     unsigned long long bytes = 0;
-    hipLaunchKernelGGL(mono_max_kernel, dim3(MONO_BLOCKS), dim3(256), 0, rs, p->ro, jobs * p->NJ, p->armtd ? 0 : jobs * (long)NF,
-                       p->d_mono_max);
-    HIPCK(hipMemcpyAsync(p->h_mono, p->d_mono_max, sizeof(p->h_mono), hipMemcpyDeviceToHost, rs));
+    if (p->lane_engine) {
+        // a copy, not a kernel: under concurrent planners a kernel here would wait for CUs another
+        // planner's reach holds, and this planner's solver with it
+        HIPCK(hipMemcpyAsync(p->h_occ, p->d_occ, sizeof(p->h_occ), hipMemcpyDeviceToHost, rs));
+    } else {
+        hipLaunchKernelGGL(mono_max_kernel, dim3(MONO_BLOCKS), dim3(256), 0, rs, p->ro, jobs * p->NJ,
+                           p->armtd ? 0 : jobs * (long)NF, p->d_mono_max);
+        HIPCK(hipMemcpyAsync(p->h_mono, p->d_mono_max, sizeof(p->h_mono), hipMemcpyDeviceToHost, rs));
+    }
     HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
     HIPCK(hipMemcpyAsync(&bytes, p->d_bytes, sizeof(bytes), hipMemcpyDeviceToHost, rs));
     HIPCK(hipStreamSynchronize(rs));
@@ -555,16 +565,19 @@ static int run_reach(armour_planner* p) {
         hipLaunchKernelGGL(lane::lane_reach_kernel, dim3((int)(bundles < g ? bundles : g)), dim3(lane::LT), 0, rs,
                            p->d_rp, la, p->ro);
         HIPCK(hipGetLastError());
-        hipLaunchKernelGGL(mono_max_kernel, dim3(MONO_BLOCKS), dim3(256), 0, rs, p->ro, jobs * p->NJ,
-                           p->armtd ? 0 : jobs * (long)NF, p->d_mono_max);
-        HIPCK(hipMemcpyAsync(p->h_mono, p->d_mono_max, sizeof(p->h_mono), hipMemcpyDeviceToHost, rs));
+        HIPCK(hipMemcpyAsync(p->h_occ, p->d_occ, sizeof(p->h_occ), hipMemcpyDeviceToHost, rs));
         HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
         HIPCK(hipStreamSynchronize(rs));
     }
-    p->mono_max[0] = p->mono_max[1] = 0;
-    for (int b = 0; b < MONO_BLOCKS; b++) {
-        p->mono_max[0] = std::max(p->mono_max[0], p->h_mono[2 * b]);
-        p->mono_max[1] = std::max(p->mono_max[1], p->h_mono[2 * b + 1]);
+    if (p->lane_engine) {
+        p->mono_max[0] = (int)std::min<unsigned long long>(p->h_occ[3], 1u << 30);
+        p->mono_max[1] = p->armtd ? 0 : (int)std::min<unsigned long long>(p->h_occ[4], 1u << 30);
+    } else {
+        p->mono_max[0] = p->mono_max[1] = 0;
+        for (int b = 0; b < MONO_BLOCKS; b++) {
+            p->mono_max[0] = std::max(p->mono_max[0], p->h_mono[2 * b]);
+            p->mono_max[1] = std::max(p->mono_max[1], p->h_mono[2 * b + 1]);
+        }
     }
     // constraint bounds from the (final) torque radii
     const long rows = (long)p->W * d.R;
