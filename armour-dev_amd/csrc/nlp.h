@@ -99,6 +99,11 @@ struct NlpDev {
     // of the list it appends to into lcount_out
     const unsigned* lcount;
     unsigned* lcount_out;
+    // sync-free tail iterations (few worlds running): ipm_world_C of round 0 also stores the running
+    // count into lrun_out (device, read as the next iteration's lcount) and nrun_flag (mapped host
+    // memory, read by the host one iteration later)
+    unsigned* lrun_out;
+    int* nrun_flag;
     // Speculative line-search round: the values (g, f) of the remaining K = max_ls - 1 trial points
     // of every world still searching after round 0, [list entry i][trial k] (eval_trials_kernel,
     // ipm_world_Cs); the trial that ends the search is then evaluated in full into the world's trial

@@ -626,7 +626,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
     static_assert(!CACHED || std::is_same<R, double>::value, "the plane cache is fp64");
     // mode 5: the trial point the speculative round chose (ipm_world_Cs: spec_k >= 0), in full,
     // into the world's trial slot (list entries, blockIdx.y -> wl)
-    if (mode == 1 && d.lcount && blockIdx.y >= *d.lcount) return;
+    if ((mode == 1 || mode == 5) && d.lcount && blockIdx.y >= *d.lcount) return;
     const int t = blockIdx.x, w = world_of(d, blockIdx.y);
     WorldState& S = d.ws[w];
     if (mode == 1 && !(S.status == 0 && S.searching)) return;
@@ -1129,6 +1129,7 @@ constexpr int UB_TS = EV_MAXK * 280;   // small variant: 9 trials of up to 280 p
 static_assert(UB_TS >= MAX_J * LM_S * 3 + NF * UM_S, "small trials staging buffer");
 template <int LM, int UM, int UB>
 __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d) {
+    if (d.lcount && blockIdx.y >= *d.lcount) return;
     const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
@@ -1502,6 +1503,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
 // point D accepts is the point A works at, so each row's value and gradient are read once; the
 // arithmetic of ipm_rows_D then ipm_rows_A. D's sums go to partial2, A's to partial.
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
+    if (d.lcount && blockIdx.y >= *d.lcount) return;
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
@@ -1645,6 +1647,7 @@ __device__ inline void world_A_body(const NlpDev& d, int w, int nside) {
 // SIMD (128 VGPRs, 2 spilled): 3.66 ms per 327-world solve against 3.95 at three. ipm_rows_DA held
 // to three spills 32 registers and slows from 6.5 to 7.9 ms, so it stays at two.
 __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void ipm_rows_B(NlpDev d) {
+    if (d.lcount && blockIdx.y >= *d.lcount) return;
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
@@ -1700,6 +1703,7 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
 }
 
 __global__ __launch_bounds__(64) void ipm_world_B(NlpDev d) {
+    if (d.lcount && blockIdx.x >= *d.lcount) return;
     const int w = world_of(d, blockIdx.x);
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
@@ -1832,6 +1836,8 @@ __global__ __launch_bounds__(64) void ipm_world_C(NlpDev d) {
         __threadfence();
         const unsigned nrun = atomicAdd(&d.cnt[0], 0u), nsearch = atomicAdd(&d.cnt[1], 0u);
         if (d.ls0) d.flags[0] = (int)nrun;
+        if (d.ls0 && d.lrun_out) *d.lrun_out = nrun;
+        if (d.ls0 && d.nrun_flag) *d.nrun_flag = (int)nrun;
         d.flags[1] = (int)nsearch;
         if (d.lcount_out) *d.lcount_out = nsearch;
         d.cnt[0] = 0;
@@ -1845,6 +1851,7 @@ __global__ __launch_bounds__(64) void ipm_world_C(NlpDev d) {
 // from the trial's own slot; the arithmetic of ipm_rows_C at that trial.
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
     const int i = blockIdx.y / d.K, k = blockIdx.y % d.K;
+    if (d.lcount && (unsigned)i >= *d.lcount) return;
     const int w = d.wl[i];
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
@@ -1873,6 +1880,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
 // list entry blockIdx.x (one wave): every trial's two partial sums at once (lane 2 k + q, block
 // partials summed in order as world_partials_at), then the acceptance tests in trial order on lane 0
 __global__ __launch_bounds__(64) void ipm_world_Cs(NlpDev d) {
+    if (d.lcount && blockIdx.x >= *d.lcount) return;
     const int i = blockIdx.x, w = d.wl[i];
     WorldState& S = d.ws[w];
     const int lane = threadIdx.x & 63;
@@ -1976,6 +1984,7 @@ __global__ __launch_bounds__(64) void ipm_world_D(NlpDev d) { world_D_body(d, wo
 __device__ inline void world_A_body(const NlpDev& d, int w, int nside);
 // the fused passes' world step: D's (of the previous iteration), then A's, one wave
 __global__ __launch_bounds__(64) void ipm_world_DA(NlpDev d, int nside) {
+    if (d.lcount && blockIdx.x >= *d.lcount) return;
     const int w = world_of(d, blockIdx.x);
     world_D_body(d, w);
     __syncthreads();  // lane 0's WorldState stores before every lane's reads in world_A_body

@@ -52,6 +52,8 @@ struct armour_planner {
     hipStream_t rstream = nullptr;   // reach phase (the planner's stream unless CUs are reserved)
     int reach_cus = 0;               // CUs the reach stream may use
     hipEvent_t ev[6];
+    hipEvent_t tev[2];        // sync-free solver tail: end of iteration it (parity it & 1)
+    int tail_worlds = 16;     // sync-free tail below this many running worlds (ARMOUR_TAIL_WORLDS, 0: off)
     // reach program (ProgramBuilder::ops) on the device
     Op* d_prog = nullptr;
     int* d_slot_off = nullptr;
@@ -177,6 +179,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         }
     }
     for (int i = 0; i < 6; i++) HIPCK(hipEventCreate(&p->ev[i]));
+    for (int i = 0; i < 2; i++) HIPCK(hipEventCreateWithFlags(&p->tev[i], hipEventDisableTiming));
+    if (const char* e = std::getenv("ARMOUR_TAIL_WORLDS")) p->tail_worlds = std::atoi(e);
     const int T = p->T, NJ = p->NJ, Om = p->Omax > 0 ? p->Omax : 1, Wm = p->Wmax;
     int rc = 0;
     if ((rc = p->alloc(&p->d_rp, 1))) return rc;
@@ -380,7 +384,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     HIPCK(hipHostMalloc((void**)&p->h_flags, 4 * sizeof(int), hipHostMallocMapped));
     HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
     // active-world lists: two per iteration (ping-pong), two per line-search round
-    if ((rc = p->alloc(&p->d_lists, 4 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 8))) return rc;
+    if ((rc = p->alloc(&p->d_lists, 4 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 12))) return rc;
     // certified plane cache: room for all 36 planes of every (link, obstacle) pair of every (world, t)
     d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
     d.pcready = 0;
@@ -398,8 +402,10 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.fs, ns)) || (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
             return rc;
     }
-    HIPCK(hipMemset(d.cnt, 0, 8 * sizeof(unsigned)));
+    HIPCK(hipMemset(d.cnt, 0, 12 * sizeof(unsigned)));
     d.lcount = nullptr;
+    d.lrun_out = nullptr;
+    d.nrun_flag = nullptr;
     d.lcount_out = nullptr;
     d.wl = nullptr;
     d.wl_run = p->d_lists;
@@ -654,10 +660,20 @@ static int run_solver(armour_planner* p) {
     // counts in mapped host memory, read after the round's one host synchronisation. Inactive
     // worlds in a list (finished by ipm_world_A / _D since) exit at once. A world's arithmetic does
     // not depend on which block serves it, so the results are those of full launches.
+    // Sync-free tail: once at most tail_worlds worlds run (and the speculative round is available),
+    // an iteration is launched without waiting for the previous one. Grids are sized by the last
+    // known running count (an upper bound: the count only falls), every launch reads the true list
+    // lengths from device memory (the running count of iteration it in cnt[8 + (it & 1)], the
+    // searching count in cnt[5]), and the host learns iteration it's running count one iteration
+    // later (event tev[it & 1], flags[2 + (it & 1)]). Blocks past a list's length exit at once, so a
+    // world's arithmetic is that of the synchronised loop.
     int cur = 0, nrun = W;
+    bool tail = false;       // iteration it - 1 ran sync-free (its running count not yet read)
     for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
+        const bool tl = it > 0 && p->spec && d.pcready && nrun <= p->tail_worlds;
         NlpDev di = d;
         di.wl = Li[cur];
+        if (tl) di.lcount = d.cnt + 8 + (it & 1);
         // pass D of the previous iteration (accept its trial point) shares one sweep over the rows
         // with this iteration's pass A
         if (it == 0) {
@@ -682,12 +698,44 @@ static int run_solver(armour_planner* p) {
             dc.wl_search = Ls[1];
             dc.ls0 = 1;
             dc.lcount_out = d.cnt + 5;
+            dc.lrun_out = d.cnt + 8 + ((it + 1) & 1);
+            if (tl) {
+                dc.lcount = di.lcount;
+                dc.nrun_flag = d.flags + 2 + (it & 1);
+            }
             launch_eval(p, dim3(p->T, nrun), dc, 1);
             hipLaunchKernelGGL(ipm_rows_C, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, dc);
             hipLaunchKernelGGL(ipm_world_C, dim3(nrun), dim3(64), 0, p->stream, dc);
-            HIPCK(hipStreamSynchronize(p->stream));
-            nnext = ((volatile int*)p->h_flags)[0];
-            nsearch = ((volatile int*)p->h_flags)[1];
+            if (!tl) {
+                HIPCK(hipStreamSynchronize(p->stream));
+                nnext = ((volatile int*)p->h_flags)[0];
+                nsearch = ((volatile int*)p->h_flags)[1];
+            }
+        }
+        if (tl) {
+            // the speculative round over at most nrun list entries, then the iteration's end event
+            NlpDev ds = d;
+            ds.wl = Ls[1];
+            ds.lcount = d.cnt + 5;
+            if (eval_small_fits(p) && d.K * p->NJ * d.O <= UB_TS)
+                hipLaunchKernelGGL(eval_trials_small, dim3(p->T, nrun), dim3(EVAL_THREADS), 0, p->stream, ds);
+            else
+                hipLaunchKernelGGL(eval_trials_kernel, dim3(p->T, nrun), dim3(EVAL_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(ipm_world_Cs, dim3(nrun), dim3(64), 0, p->stream, ds);
+            launch_eval(p, dim3(p->T, nrun), ds, 5);
+            HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
+            HIPCK(hipGetLastError());
+            cur = 1 - cur;
+            if (tail) {
+                // iteration it - 1's running count: the worlds iteration it was launched for
+                HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
+                const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
+                if (prev == 0) break;  // iteration it had nothing to do
+                nrun = prev < nrun ? prev : nrun;
+            }
+            tail = true;
+            continue;
         }
         if (nsearch > 0 && p->spec && d.pcready) {
             // the worlds still searching: the values of all remaining trials at once, the acceptance
@@ -858,6 +906,7 @@ void armour_destroy(armour_planner* p) {
     if (p->h_feas) (void)hipHostFree(p->h_feas);
     if (p->stream) {
         for (int i = 0; i < 6; i++) (void)hipEventDestroy(p->ev[i]);
+        for (int i = 0; i < 2; i++) (void)hipEventDestroy(p->tev[i]);
         if (p->rstream && p->rstream != p->stream) (void)hipStreamDestroy(p->rstream);
         (void)hipStreamDestroy(p->stream);
     }
