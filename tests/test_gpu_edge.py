@@ -114,3 +114,29 @@ def test_speculative_line_search_matches_sequential():
         assert (a["iterations"], a["evaluations"], a["status"], a["feasible"]) == \
             (b["iterations"], b["evaluations"], b["status"], b["feasible"])
         assert np.array_equal(g_s[w], Q.constraints(w)) and np.array_equal(c_s[w], Q.link_centers(w))
+
+
+@pytest.mark.parametrize("tail", ["1000", "16"])
+def test_sync_free_tail_matches_synchronised(tail):
+    """Sync-free tail iterations (planner.hip run_solver: bounded grids, device-side list lengths,
+    the running count read one iteration later) give bitwise the plans of the loop synchronised
+    every iteration (ARMOUR_TAIL_WORLDS=0). "1000" runs every iteration after the first sync-free;
+    also one world alone, the drop-in's batch."""
+    import os
+
+    T, O = 40, 10
+    for worlds in ([A.make_world(s, O, profile="survey") for s in range(48)], [A.make_world(7, O, profile="survey")]):
+        planners = []
+        for tw in ("0", tail):
+            os.environ["ARMOUR_TAIL_WORLDS"] = tw
+            try:
+                planners.append(A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds)))
+            finally:
+                del os.environ["ARMOUR_TAIL_WORLDS"]
+        (res_s, _), (res_t, _) = [P.plan(worlds) for P in planners]
+        for w, (a, b) in enumerate(zip(res_s, res_t)):
+            assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"]
+            assert (a["iterations"], a["evaluations"], a["status"], a["feasible"]) == \
+                (b["iterations"], b["evaluations"], b["status"], b["feasible"])
+            assert np.array_equal(planners[0].constraints(w), planners[1].constraints(w))
+            assert np.array_equal(planners[0].link_centers(w), planners[1].link_centers(w))
