@@ -1578,14 +1578,14 @@ __device__ inline void world_partials_at(const double* base, int nblk, int strid
     for (int q = 0; q < N; q++)
         if (q == lane) { s = init[q]; o = op[q]; }
     if (lane < N) {
-        // eight block partials in flight per step (clamped loads), combined in block order
+        // sixteen block partials in flight per step (clamped loads), combined in block order
         const double* in = base + lane;
-        for (int b0 = 0; b0 < nblk; b0 += 8) {
-            double x[8];
+        for (int b0 = 0; b0 < nblk; b0 += 16) {
+            double x[16];
 #pragma unroll
-            for (int u = 0; u < 8; u++) x[u] = in[(long)min(b0 + u, nblk - 1) * stride];
+            for (int u = 0; u < 16; u++) x[u] = in[(long)min(b0 + u, nblk - 1) * stride];
 #pragma unroll
-            for (int u = 0; u < 8; u++)
+            for (int u = 0; u < 16; u++)
                 if (b0 + u < nblk) s = o == 0 ? s + x[u] : o == 1 ? fmax(s, x[u]) : fmin(s, x[u]);
         }
     }
@@ -1893,12 +1893,12 @@ __global__ __launch_bounds__(64) void ipm_world_Cs(NlpDev d) {
     if (lane < 2 * d.K) {
         const double* in = d.partial_s + ((long)i * d.K + (lane >> 1)) * d.nblk * KA + (lane & 1);
         const int nb = d.nblk;
-        for (int b0 = 0; b0 < nb; b0 += 8) {
-            double x[8];
+        for (int b0 = 0; b0 < nb; b0 += 16) {
+            double x[16];
 #pragma unroll
-            for (int u = 0; u < 8; u++) x[u] = in[(long)min(b0 + u, nb - 1) * KA];
+            for (int u = 0; u < 16; u++) x[u] = in[(long)min(b0 + u, nb - 1) * KA];
 #pragma unroll
-            for (int u = 0; u < 8; u++)
+            for (int u = 0; u < 16; u++)
                 if (b0 + u < nb) s = s + x[u];
         }
     }
