@@ -108,15 +108,32 @@ def start_obstacle(robot_geo, q0, rng):
     return _box(cs[l], half)
 
 
-def boundary_world(seed, kind, T, O, threads=8, robot=KINOVA, n_tuned=None, t_lo=0.5):
+ROBOTS = ("kinova", "fetch")
+
+
+def robot_of(name="kinova"):
+    """(geometry for the world generator, armour_robot struct for the oracle or None, tables or
+    None) of a fixture's robot: "kinova" = the built-in KPR/KinovaWithoutGripperInfo.h tables,
+    "fetch" = tests/golden/robot_fetch.json (the Fetch arm from its URDF, 8 joints)"""
+    if name == "kinova":
+        return KINOVA, None, None
+    import os
+
+    from armour_amd import robot_tables as RT
+    tables = RT.load_json(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "robot_fetch.json"))
+    return RT.geometry(tables), RT.to_struct(tables), tables
+
+
+def boundary_world(seed, kind, T, O, threads=8, robot=KINOVA, n_tuned=None, t_lo=0.5, robot_struct=None):
     """one decision-boundary world (q0, qd0, qdd0, q_des, obstacles[O, 12]) plus the x0 it is tuned at.
     n_tuned obstacles are tuned near the threshold (default: half of them for graze kinds, a quarter otherwise);
-    the rest come from the ordinary generator."""
+    the rest come from the ordinary generator. robot: the generator's geometry; robot_struct: the
+    oracle's armour_robot tables (None: Kinova)."""
     rng = np.random.default_rng(10_000 + seed)
     q0, qd0, qdd0, q_des = start_state(rng, kind, robot)
     x0 = np.zeros(7)
     filler = make_world(seed, O, robot=robot)[4]
-    R = OraclePlanner(q0, qd0, qdd0, q_des, filler, T=T, threads=threads)
+    R = OraclePlanner(q0, qd0, qdd0, q_des, filler, T=T, threads=threads, robot=robot_struct)
     R.reach()
     NJ = R.NJ
     _, _, lc = R.eval(x0, centers=True)

@@ -30,21 +30,27 @@ from oracle import OraclePlanner  # noqa: E402
 OUT = os.path.dirname(os.path.abspath(__file__))
 PATTERN = ["graze", "graze", "graze_moving", "graze_moving", "graze", "torque", "start", "graze"]
 
-# name -> (T, O, number of worlds, kinds, tuned obstacles per graze world (None: half))
+# name -> (T, O, number of worlds, kinds, tuned obstacles per graze world (None: half), robot)
 SETS = {
-    "boundary_small_T20_O6": (20, 6, 12, PATTERN, None),
-    "boundary_config2_T100_O20": (100, 20, 16, PATTERN, None),
-    "boundary_config3_T200_O40": (200, 40, 6, ["graze", "graze_moving", "start", "torque", "graze", "graze"], 8),
+    "boundary_small_T20_O6": (20, 6, 12, PATTERN, None, "kinova"),
+    "boundary_config2_T100_O20": (100, 20, 16, PATTERN, None, "kinova"),
+    "boundary_config3_T200_O40": (200, 40, 6, ["graze", "graze_moving", "start", "torque", "graze", "graze"], 8, "kinova"),
+    # config 5's robot (the Fetch arm from its URDF, 8 links) on the decision boundary, at fp64
+    "boundary_fetch_T100_O20": (100, 20, 16, PATTERN, None, "fetch"),
+    # the drop-in's horizon: NUM_TIME_STEPS = 128 (KPR/Parameters.h:17), armour_main's default
+    "boundary_dropin_T128_O20": (128, 20, 8, PATTERN, None, "kinova"),
 }
 
 
-def make_set(name, T, O, n, kinds, tuned):
+def make_set(name, T, O, n, kinds, tuned, robot="kinova"):
+    geo, rs, _ = B.robot_of(robot)
     rec = {k: [] for k in ("kinds", "q0", "qd0", "qdd0", "q_des", "obstacles", "x0", "feasible", "status",
                            "iterations", "k_opt", "cost", "near_x0", "near_kopt", "dec_x0", "feasible_x0")}
     for s in range(n):
         kind = kinds[s % len(kinds)]
-        world, x0 = B.boundary_world(s, kind, T, O, n_tuned=tuned if kind.startswith("graze") else None)
-        R = OraclePlanner(*world, T=T, threads=8)
+        world, x0 = B.boundary_world(s, kind, T, O, robot=geo, robot_struct=rs,
+                                     n_tuned=tuned if kind.startswith("graze") else None)
+        R = OraclePlanner(*world, T=T, threads=8, robot=rs)
         R.reach()
         NJ = R.NJ
         g0 = R.eval(x0, jac=False)
@@ -68,6 +74,7 @@ def make_set(name, T, O, n, kinds, tuned):
               f"near@x0={rec['near_x0'][-1]:4d} near@kopt={rec['near_kopt'][-1]:4d}", flush=True)
     out = {k: np.array(v) for k, v in rec.items()}
     out["T"] = np.int64(T)
+    out["robot"] = np.array(robot)
     np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
     return out
 
@@ -75,12 +82,12 @@ def make_set(name, T, O, n, kinds, tuned):
 def main():
     summary = {}
     only = sys.argv[1:]
-    for name, (T, O, n, kinds, tuned) in SETS.items():
+    for name, (T, O, n, kinds, tuned, robot) in SETS.items():
         if only and name not in only:
             continue
         t0 = time.time()
-        out = make_set(name, T, O, n, kinds, tuned)
-        summary[name] = dict(T=T, O=O, worlds=n, infeasible=int((~out["feasible"]).sum()),
+        out = make_set(name, T, O, n, kinds, tuned, robot)
+        summary[name] = dict(T=T, O=O, worlds=n, robot=robot, infeasible=int((~out["feasible"]).sum()),
                              near_threshold_rows_x0=int(out["near_x0"].sum()),
                              near_threshold_rows_kopt=int(out["near_kopt"].sum()),
                              seconds=round(time.time() - t0, 1))

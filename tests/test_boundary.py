@@ -21,10 +21,14 @@ def world(fx, w):
     return fx["q0"][w], fx["qd0"][w], fx["qdd0"][w], fx["q_des"][w], fx["obstacles"][w]
 
 
+def robot_name(fx):
+    return str(fx["robot"]) if "robot" in fx else "kinova"
+
+
 def check_world(fx, w, threads=4):
     T = int(fx["T"])
     O = fx["obstacles"].shape[1]
-    R = OraclePlanner(*world(fx, w), T=T, threads=threads)
+    R = OraclePlanner(*world(fx, w), T=T, threads=threads, robot=B.robot_of(robot_name(fx))[1])
     R.reach()
     g0 = R.eval(fx["x0"][w], jac=False)
     col = g0[B.collision_slice(T, R.NJ, O)]
@@ -48,7 +52,23 @@ def test_config2_set_reproduced(w):
     check_world(load("boundary_config2_T100_O20"), w, threads=8)
 
 
-@pytest.mark.parametrize("name", ["boundary_small_T20_O6", "boundary_config2_T100_O20", "boundary_config3_T200_O40"])
+@pytest.mark.parametrize("w", [0, 2, 6])
+def test_fetch_set_reproduced(w):
+    """config 5's robot (Fetch, 8 links) on the decision boundary: graze, moving graze, start"""
+    check_world(load("boundary_fetch_T100_O20"), w, threads=8)
+
+
+@pytest.mark.parametrize("w", [0, 5])
+def test_dropin_horizon_set_reproduced(w):
+    """T = 128, the reference's NUM_TIME_STEPS (KPR/Parameters.h:17)"""
+    check_world(load("boundary_dropin_T128_O20"), w, threads=8)
+
+
+SETS = ["boundary_small_T20_O6", "boundary_config2_T100_O20", "boundary_config3_T200_O40", "boundary_fetch_T100_O20",
+        "boundary_dropin_T128_O20"]
+
+
+@pytest.mark.parametrize("name", SETS)
 def test_fixture_sits_on_the_decisions(name):
     fx = load(name)
     feas = fx["feasible"]
@@ -59,9 +79,10 @@ def test_fixture_sits_on_the_decisions(name):
     if name != "boundary_small_T20_O6":
         assert fx["near_x0"].sum() + fx["near_kopt"].sum() >= 1000
     # graze worlds: some collision decisions at x0 are violations, most rows are clear
+    NJ = 8 if robot_name(fx) == "fetch" else 7
     for w in np.where(kinds == "graze")[0]:
         T, O = int(fx["T"]), fx["obstacles"].shape[1]
-        bits = np.unpackbits(fx["dec_x0"][w])[: 7 * T * O]
+        bits = np.unpackbits(fx["dec_x0"][w])[: NJ * T * O]
         assert bits.mean() < 0.05
 
 

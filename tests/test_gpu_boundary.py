@@ -18,7 +18,7 @@ import armour_amd as A
 import boundary_worlds as B
 from conftest import engine
 from oracle import OraclePlanner
-from test_boundary import load, world
+from test_boundary import load, robot_name, world
 from test_gpu_drop_in import run, write_input
 
 pytestmark = pytest.mark.gpu
@@ -29,13 +29,14 @@ def compare_set(name, min_near, eng):
     fx = load(name)
     T, W, O = int(fx["T"]), len(fx["kinds"]), fx["obstacles"].shape[1]
     worlds = [world(fx, w) for w in range(W)]
+    _, rstruct, tables = B.robot_of(robot_name(fx))
     with engine(eng):
-        P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+        P = A.Planner(T=T, max_obstacles=O, max_worlds=W, robot=tables)
     P.reach(worlds)
     near = 0
     refs = []
     for w in range(W):
-        R = OraclePlanner(*worlds[w], T=T, threads=8)
+        R = OraclePlanner(*worlds[w], T=T, threads=8, robot=rstruct)
         R.reach()
         refs.append(R)
         np.testing.assert_allclose(P.torque_radius(w), R.torque_radius(), rtol=0, atol=TOL)
@@ -95,6 +96,21 @@ def test_boundary_config3(eng):
     """BASELINE configs[2] sizes (T=200, O=40) on the decision boundary"""
     near, infeasible = compare_set("boundary_config3_T200_O40", 1000, eng)
     print(f"config 3 boundary ({eng}): {near} near-threshold rows compared, {infeasible} infeasible plans")
+
+
+def test_boundary_fetch():
+    """BASELINE configs[4]'s robot (the Fetch arm from its URDF, all 8 links' collision rows) on the
+    decision boundary at T=100, O=20, fp64. Its reach program does not fit the per-job engine's LDS
+    pool, so only the bundle engine runs it (planner.hip job_fits)."""
+    near, infeasible = compare_set("boundary_fetch_T100_O20", 1000, "lane")
+    print(f"Fetch boundary: {near} near-threshold rows compared, {infeasible} infeasible plans")
+
+
+@pytest.mark.parametrize("eng", ENGINES)
+def test_boundary_dropin_horizon(eng):
+    """the drop-in's T = 128 (KPR/Parameters.h:17, armour_main's default) on the decision boundary"""
+    near, infeasible = compare_set("boundary_dropin_T128_O20", 1000, eng)
+    print(f"T=128 boundary ({eng}): {near} near-threshold rows compared, {infeasible} infeasible plans")
 
 
 def test_drop_in_writes_minus_one_for_infeasible(tmp_path):

@@ -1,0 +1,90 @@
+"""Solver fidelity beyond the oracle it mirrors (VERDICT r02 "What's weak" 6).
+
+armour-IPM stands in for Ipopt (KPR/armour_main.cu:238-290; Ipopt + MA97 are not in this image).
+Its CPU statement (oracle/src/ipm.cpp) and the GPU solver agree path for path (the GPU suites),
+so these checks hold the *answers* to an independent optimiser, scipy's SLSQP (an active-set SQP:
+a different algorithm from an interior point), on the reference's NLP as the oracle evaluates it
+(cost NLPclass.cu:207-267, constraints :272-396, bounds :87-165), on the headline workload's worlds
+(tests/golden/bench_survey_T100_O20.npz):
+
+  * a converged plan is a local optimum: SLSQP started at k_opt finds no point more than 5e-4
+    better in the NLP objective (an interior point stops at barrier parameter ~tol / 10 with
+    slack ~mu / z left on the active constraints; measured gap <= 1.4e-4 over 60 worlds);
+  * an infeasible verdict is not a solver failure: minimising the largest constraint violation
+    (phase 1) with SLSQP from x = 0 and random starts never gets below the reference's violation
+    thresholds (KPR/Parameters.h:38,41).
+"""
+import numpy as np
+import pytest
+from scipy.optimize import minimize
+
+from oracle import OraclePlanner
+from test_bench_worlds import bench_world, load
+
+K_GAP = 5e-4
+
+
+def _problem(fx, i):
+    R = OraclePlanner(*bench_world(fx, i), T=int(fx["T"]), threads=8)
+    R.reach()
+    gl, gu = R.bounds()
+    lo, hi = np.abs(gl) < 1e19, np.abs(gu) < 1e19
+    memo = {}
+
+    def ev(x):
+        k = x.tobytes()
+        if k not in memo:
+            memo.clear()
+            memo[k] = R.eval(x)
+        return memo[k]
+
+    def cons(x):
+        g = ev(x)[0]
+        return np.concatenate([g[lo] - gl[lo], gu[hi] - g[hi]])
+
+    def jac(x):
+        J = ev(x)[1]
+        return np.concatenate([J[lo], -J[hi]])
+
+    return R, cons, jac
+
+
+CONVERGED = [1, 4, 8, 27, 47, 61]
+INFEASIBLE = [0, 17, 24, 35]
+
+
+@pytest.mark.parametrize("i", CONVERGED)
+def test_converged_plan_is_a_local_optimum(i):
+    fx = load()
+    assert fx["status"][i] == 0 and fx["feasible"][i]
+    R, cons, jac = _problem(fx, i)
+    x0 = fx["k_opt"][i]
+    f0 = R.cost(x0)[0]
+    r = minimize(lambda x: R.cost(x)[0], x0, jac=lambda x: R.cost(x)[1], bounds=[(-1, 1)] * 7,
+                 constraints=[dict(type="ineq", fun=cons, jac=jac)], method="SLSQP",
+                 options=dict(maxiter=300, ftol=1e-12))
+    assert r.success, r.message
+    assert -cons(r.x).min() <= 1e-9, "SLSQP's point must be feasible to compare"
+    print(f"world {i}: f(k_opt) {f0:.6e}, SLSQP {r.fun:.6e}, gap {f0 - r.fun:.2e}")
+    assert f0 - r.fun <= K_GAP
+
+
+@pytest.mark.parametrize("i", INFEASIBLE)
+def test_infeasible_verdict_has_no_feasible_point(i):
+    fx = load()
+    assert not fx["feasible"][i]
+    R, cons, jac = _problem(fx, i)
+    n = cons(np.zeros(7)).size
+    # phase 1: min t subject to cons(x) + t >= 0, x in the box
+    best = np.inf
+    rng = np.random.default_rng(i)
+    for x0 in [np.zeros(7)] + [rng.uniform(-1, 1, 7) for _ in range(3)]:
+        t0 = max(0.0, -cons(x0).min())
+        r = minimize(lambda z: z[7], np.append(x0, t0), jac=lambda z: np.eye(8)[7],
+                     bounds=[(-1, 1)] * 7 + [(0, None)],
+                     constraints=[dict(type="ineq", fun=lambda z: cons(z[:7]) + z[7],
+                                       jac=lambda z: np.hstack([jac(z[:7]), np.ones((n, 1))]))],
+                     method="SLSQP", options=dict(maxiter=300, ftol=1e-12))
+        best = min(best, max(0.0, -cons(r.x[:7]).min()))
+    print(f"world {i}: least largest violation found {best:.3e}")
+    assert best > 1e-2  # above both thresholds (torque 1e-2, collision 1e-4)
