@@ -37,6 +37,7 @@ struct LaneArgs {
     unsigned long long* btime; // optional [bundles][2]: start / end wall clock of every bundle
     unsigned long long* occ;   // [8] largest use over the launch: arena hashes, arena rows, operator
                                // terms, link / torque k-only monomials (capacity headroom)
+    ReachCounters rc;          // rc.occ == occ, rc.bytes == bytes; published by the last workgroup
     const int* wlist;      // null: every world of the batch; else only these worlds (a retry)
     int nlist;
 };
@@ -59,6 +60,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     __shared__ LArena arena;
     __shared__ int err;
     __shared__ int occ[4];
+    __shared__ int last;
 
     const RobotParams& rp = *rpp;
     const long wg = blockIdx.x;
@@ -129,6 +131,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
         }
         __syncthreads();
     }
+    publish_counters(a.rc, out.err, a.W, &last);
 }
 
 }  // namespace lane

@@ -239,13 +239,11 @@ __device__ inline __attribute__((always_inline)) R slice_term(R co, int h, int k
 }
 
 // ------------------------------------------------------------------------------------------
-// constraint bounds (NLPclass.cu:87-165); rows m..m+NF-1 are the box bounds on x
-__global__ void bounds_kernel(NlpDev d) {
+// constraint bounds (NLPclass.cu:87-165) of row r of world w; rows m..m+NF-1 are the box bounds on
+// x. Formed by ipm_rows_init on the solver stream (no kernel of its own on the reach stream).
+__device__ inline void bounds_of(const NlpDev& d, int w, int r, double& L, double& U) {
     const RobotParams& rp = *d.rp;
-    const long total = (long)d.W * d.R;
-    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-        const int w = (int)(idx / d.R), r = (int)(idx % d.R);
-        double L, U;
+    {
         const int nt = d.nt, nc = d.T * d.NJ * d.O;
         if (r < nt) {
             const int t = r / NF, j = r % NF;
@@ -265,8 +263,6 @@ __global__ void bounds_kernel(NlpDev d) {
         } else {
             L = -1.0; U = 1.0;  // NLPclass.cu:105-113
         }
-        d.L[idx] = L;
-        d.U[idx] = U;
     }
 }
 
@@ -1305,33 +1301,6 @@ __global__ __launch_bounds__(EVAL_THREADS) __attribute__((amdgpu_waves_per_eu(5,
     eval_trials_body<LM_S, UM_S, UB_TS>(d);
 }
 
-// the largest link / torque k-monomial counts of a reach (nt = 0: no torque PZs): block b writes
-// the maxima of its grid-stride slice to out[2 b], out[2 b + 1]; the host takes the max over blocks
-// and picks the evaluation kernels' LDS capacities from them
-constexpr int MONO_BLOCKS = 64;
-__global__ __launch_bounds__(256) void mono_max_kernel(ReachOut ro, long nl, long nt, int* out) {
-    int ml = 0, mt = 0;
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) ml = max(ml, ro.link_cnt[i]);
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += stride) mt = max(mt, ro.tq_cnt[i]);
-    __shared__ int r[2][4];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        ml = max(ml, __shfl_xor(ml, off));
-        mt = max(mt, __shfl_xor(mt, off));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        r[0][threadIdx.x >> 6] = ml;
-        r[1][threadIdx.x >> 6] = mt;
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) {
-        int m = 0;
-        for (int k = 0; k < (int)(blockDim.x >> 6); k++) m = max(m, r[threadIdx.x][k]);
-        out[2 * blockIdx.x + threadIdx.x] = m;
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // armour-IPM
 __global__ __launch_bounds__(64) void ipm_world_init(NlpDev d) {
@@ -1371,7 +1340,9 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
         const double v = row_va(d, S.cur, w, (int)r, S.x, a);
         const long i = (long)w * d.R + r;
         double L, U;
-        row_bounds(d, i, (int)r, L, U);
+        bounds_of(d, w, (int)r, L, U);
+        d.L[i] = L;
+        d.U[i] = U;
         const bool hl = has_lo(d, L), hh = has_hi(d, U);
         double p = 0;
         if (hl && hh) p = fmin(d.opt.bound_push * fmax(1.0, fabs(L)), d.opt.bound_push * (U - L));

@@ -63,7 +63,10 @@ struct armour_planner {
     unsigned long long* d_prof = nullptr;  // per-op [cycles, terms] when ARMOUR_PROFILE_OPS is set
     double* d_dump = nullptr;              // op-by-op state of job 0 when ARMOUR_DUMP_OPS is set
     double last_kernel_ms = 0, last_bytes = 0;
-    unsigned long long* d_occ = nullptr;   // [8] reach capacity use of the last batch (lane kernel)
+    unsigned long long* d_occ = nullptr;   // [8] reach capacity use of the last launch (ReachCounters)
+    unsigned* d_done = nullptr;            // workgroups finished in the current reach launch
+    long long* h_sum = nullptr;            // mapped host: reach counters published by the last workgroup
+    ReachCounters rc{};                    // (reach_kernel.hip)
     int* d_wlist = nullptr;                // [max_worlds] worlds of a capacity retry
     int last_retried = 0, last_failed = 0;
     std::vector<int> world_err;            // per world of the last batch: 0 or ARMOUR_E_CAPACITY
@@ -81,11 +84,8 @@ struct armour_planner {
     bool job_fits = true;     // the reach program's payload pool fits the per-job engine's LDS
     bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
     bool eval_full = false;   // ARMOUR_EVAL_FULL: always the full-capacity evaluation kernels
-    // largest link / torque k-monomial counts of the last reach: the bundle engine records them
-    // (d_occ[3], d_occ[4], copied with the error flags); the per-job engine's batches take
-    // mono_max_kernel's per-block maxima [MONO_BLOCKS][2]
-    int* d_mono_max = nullptr;
-    int h_mono[2 * MONO_BLOCKS] = {};
+    // largest link / torque k-monomial counts of the last reach (both engines record them in
+    // occ[3], occ[4], published with the error flags), and the first launch's occupancy
     unsigned long long h_occ[8] = {};
     int mono_max[2] = {CAP_LM, CAP_UM};
     int lane_grid = 0;
@@ -277,7 +277,16 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         HIPCK(hipMemset(p->d_dump, 0, sizeof(double) * p->nops * DUMP_W));
         ra.dump = p->d_dump;
     }
-    if ((rc = p->alloc(&p->d_jrs, jobs * NF)) || (rc = p->alloc(&p->d_mono_max, 2 * MONO_BLOCKS))) return rc;
+    if ((rc = p->alloc(&p->d_jrs, jobs * NF)) || (rc = p->alloc(&p->d_occ, 8)) || (rc = p->alloc(&p->d_done, 1))) return rc;
+    HIPCK(hipMemset(p->d_done, 0, sizeof(unsigned)));
+    {
+        long long* dsum = nullptr;
+        HIPCK(hipHostMalloc((void**)&p->h_sum, sizeof(long long) * (RSUM_ERR + (size_t)Wm), hipHostMallocMapped));
+        HIPCK(hipHostGetDevicePointer((void**)&dsum, p->h_sum, 0));
+        p->rc = ReachCounters{p->d_bytes, p->d_occ, p->d_done, dsum};
+        ra.rc = p->rc;
+        ra.ntq = p->armtd ? 0 : NF;
+    }
     {
         const char* f32 = std::getenv("ARMOUR_EVAL_F32");
         p->eval_f32 = f32 && std::atoi(f32) != 0;
@@ -322,8 +331,9 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             (rc = p->alloc(&la.gkp, G * (la.gcap + 1))) || (rc = p->alloc(&la.ggp, G * (la.gcap + 1))) ||
             (rc = p->alloc(&la.gout, G * la.ocap * 9 * LGs)) || (rc = p->alloc(&la.gm, G * la.ocap)))
             return rc;
-        if ((rc = p->alloc(&p->d_occ, 8)) || (rc = p->alloc(&p->d_wlist, (size_t)Wm))) return rc;
+        if ((rc = p->alloc(&p->d_wlist, (size_t)Wm))) return rc;
         la.occ = p->d_occ;
+        la.rc = p->rc;
         la.wlist = nullptr;
         la.nlist = 0;
         la.prog = p->d_prog;
@@ -484,11 +494,13 @@ static int upload_armtd(armour_planner* p, int W, const armour_armtd_world* worl
     return upload_worlds(p, W, base.data());  // ends in a synchronisation: tab / kr outlive the copies
 }
 
-// reach set + bounds for the uploaded batch
+// reach set for the uploaded batch. The whole phase is three kernel launches on the reach stream
+// (JRS, reach, and a capacity retry when needed) and one event wait: jrs_kernel zeroes the
+// counters, the reach kernel's last workgroup publishes them in mapped host memory
+// (ReachCounters), and the constraint bounds are formed by the solver's ipm_rows_init. Nothing
+// else is queued here, so under concurrent planners no small kernel waits for CUs another
+// planner's persistent reach kernel holds.
 static int run_reach(armour_planner* p) {
-    NlpDev& d = p->d;
-    // the reach phase on the reach stream (ordered after the uploads, which end in a host
-    // synchronisation of the planner stream; it ends in one itself)
     hipStream_t rs = p->rstream;
     ReachArgs ra = p->ra;
     ra.W = p->W;
@@ -496,9 +508,6 @@ static int run_reach(armour_planner* p) {
     ra.q0 = p->q0;
     ra.qd0 = p->qd0;
     ra.qdd0 = p->qdd0;
-    HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, rs));
-    HIPCK(hipMemsetAsync(p->d_bytes, 0, sizeof(unsigned long long), rs));
-    if (p->d_occ) HIPCK(hipMemsetAsync(p->d_occ, 0, sizeof(unsigned long long) * 8, rs));
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
     p->lane_engine = !(p->has_job && jobs <= p->job_max);
@@ -506,10 +515,10 @@ static int run_reach(armour_planner* p) {
     HIPCK(hipEventRecord(p->ev[3], rs));
     if (p->armtd)
         hipLaunchKernelGGL(jrs_armtd_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, rs, p->W, p->T, p->q0, p->d_tables,
-                           p->d_jrs);
+                           p->d_jrs, p->rc, p->ro.err);
     else
         hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
-                           p->qdd0, p->d_jrs);
+                           p->qdd0, p->d_jrs, p->rc, p->ro.err);
     ra.jrs = p->d_jrs;
     if (p->lane_engine) {
         lane::LaneArgs la = p->la;
@@ -524,34 +533,27 @@ static int run_reach(armour_planner* p) {
     }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(p->ev[4], rs));
+    HIPCK(hipEventSynchronize(p->ev[4]));
+    const volatile long long* sum = p->h_sum;
     std::vector<int> err(p->W);
-    unsigned long long bytes = 0;
-    if (p->lane_engine) {
-        // a copy, not a kernel: under concurrent planners a kernel here would wait for CUs another
-        // planner's reach holds, and this planner's solver with it
-        HIPCK(hipMemcpyAsync(p->h_occ, p->d_occ, sizeof(p->h_occ), hipMemcpyDeviceToHost, rs));
-    } else {
-        hipLaunchKernelGGL(mono_max_kernel, dim3(MONO_BLOCKS), dim3(256), 0, rs, p->ro, jobs * p->NJ,
-                           p->armtd ? 0 : jobs * (long)NF, p->d_mono_max);
-        HIPCK(hipMemcpyAsync(p->h_mono, p->d_mono_max, sizeof(p->h_mono), hipMemcpyDeviceToHost, rs));
-    }
-    HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
-    HIPCK(hipMemcpyAsync(&bytes, p->d_bytes, sizeof(bytes), hipMemcpyDeviceToHost, rs));
-    HIPCK(hipStreamSynchronize(rs));
+    for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
+    for (int k = 0; k < 8; k++) p->h_occ[k] = (unsigned long long)sum[1 + k];
     {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, p->ev[3], p->ev[4]);
         p->last_kernel_ms = ms;
-        p->last_bytes = (double)bytes;
+        p->last_bytes = (double)sum[0];
     }
     // Capacity isolation. A bundle that overflowed its arena / key buffers flags every world it
     // holds. Those worlds' jobs run again in a second launch of a quarter of the workgroups, each
     // with four workgroups' buffers (4x the arena, key and output capacity). A world that still
     // overflows gets ARMOUR_E_CAPACITY in its result and is not planned; the batch goes on.
+    // (armour_get_reach_occupancy reports the first launch against its 1x capacities: h_occ.)
     std::vector<int> retry;
     for (int w = 0; w < p->W; w++)
         if (err[w]) retry.push_back(w);
     p->last_retried = (int)retry.size();
+    unsigned long long mono[2] = {p->h_occ[3], p->h_occ[4]};
     if (!retry.empty() && p->lane_engine) {
         lane::LaneArgs la = p->la;
         la.W = p->W;
@@ -564,6 +566,8 @@ static int run_reach(armour_planner* p) {
         la.pool_rows *= RETRY_SCALE;
         la.wlist = p->d_wlist;
         la.nlist = (int)retry.size();
+        la.dump = nullptr;   // the op dump and bundle times stay those of the first launch
+        la.btime = nullptr;
         HIPCK(hipMemcpyAsync(p->d_wlist, retry.data(), sizeof(int) * retry.size(), hipMemcpyHostToDevice, rs));
         HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, rs));
         const long bundles = ((long)retry.size() * p->T + lane::LG - 1) / lane::LG;
@@ -571,24 +575,14 @@ static int run_reach(armour_planner* p) {
         hipLaunchKernelGGL(lane::lane_reach_kernel, dim3((int)(bundles < g ? bundles : g)), dim3(lane::LT), 0, rs,
                            p->d_rp, la, p->ro);
         HIPCK(hipGetLastError());
-        HIPCK(hipMemcpyAsync(p->h_occ, p->d_occ, sizeof(p->h_occ), hipMemcpyDeviceToHost, rs));
-        HIPCK(hipMemcpyAsync(err.data(), p->ro.err, sizeof(int) * p->W, hipMemcpyDeviceToHost, rs));
-        HIPCK(hipStreamSynchronize(rs));
+        HIPCK(hipEventRecord(p->ev[5], rs));
+        HIPCK(hipEventSynchronize(p->ev[5]));
+        for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
+        mono[0] = (unsigned long long)sum[1 + 3];   // maxima over both launches (occ accumulates)
+        mono[1] = (unsigned long long)sum[1 + 4];
     }
-    if (p->lane_engine) {
-        p->mono_max[0] = (int)std::min<unsigned long long>(p->h_occ[3], 1u << 30);
-        p->mono_max[1] = p->armtd ? 0 : (int)std::min<unsigned long long>(p->h_occ[4], 1u << 30);
-    } else {
-        p->mono_max[0] = p->mono_max[1] = 0;
-        for (int b = 0; b < MONO_BLOCKS; b++) {
-            p->mono_max[0] = std::max(p->mono_max[0], p->h_mono[2 * b]);
-            p->mono_max[1] = std::max(p->mono_max[1], p->h_mono[2 * b + 1]);
-        }
-    }
-    // constraint bounds from the (final) torque radii
-    const long rows = (long)p->W * d.R;
-    hipLaunchKernelGGL(bounds_kernel, dim3((int)((rows + 255) / 256)), dim3(256), 0, rs, d);
-    HIPCK(hipGetLastError());
+    p->mono_max[0] = (int)std::min<unsigned long long>(mono[0], 1u << 30);
+    p->mono_max[1] = p->armtd ? 0 : (int)std::min<unsigned long long>(mono[1], 1u << 30);
     p->world_err.assign(p->W, 0);
     p->last_failed = 0;
     for (int w = 0; w < p->W; w++)
@@ -901,6 +895,7 @@ void armour_destroy(armour_planner* p) {
     if (p->stream) (void)hipStreamSynchronize(p->stream);
     for (void* a : p->allocs) (void)hipFree(a);
     if (p->h_flags) (void)hipHostFree(p->h_flags);
+    if (p->h_sum) (void)hipHostFree(p->h_sum);
     if (p->h_ws) (void)hipHostFree(p->h_ws);
     if (p->h_f) (void)hipHostFree(p->h_f);
     if (p->h_feas) (void)hipHostFree(p->h_feas);
@@ -964,9 +959,9 @@ int armour_plan_armtd_batch(armour_planner* p, int W, const armour_armtd_world* 
 
 static int reach_uploaded(armour_planner* p, armour_timing* timing, std::chrono::steady_clock::time_point t0) {
     int rc = 0;
-    HIPCK(hipEventRecord(p->ev[0], p->stream));
+    HIPCK(hipEventRecord(p->ev[0], p->rstream));
     if ((rc = run_reach(p))) return rc;
-    HIPCK(hipEventRecord(p->ev[1], p->stream));
+    HIPCK(hipEventRecord(p->ev[1], p->rstream));
     HIPCK(hipEventSynchronize(p->ev[1]));
     if (timing) {
         float ms = 0;
@@ -994,9 +989,11 @@ static int plan_uploaded(armour_planner* p, armour_result* results, armour_timin
                          std::chrono::steady_clock::time_point t0) {
     int rc = 0;
     const int W = p->W;
-    HIPCK(hipEventRecord(p->ev[0], p->stream));
+    // the reach phase on the reach stream (ev[0] .. ev[1]; run_reach ends in a host wait for it),
+    // then the solver on the planner's stream (ev[1] .. ev[2])
+    HIPCK(hipEventRecord(p->ev[0], p->rstream));
     if ((rc = run_reach(p))) return rc;
-    HIPCK(hipEventRecord(p->ev[1], p->stream));
+    HIPCK(hipEventRecord(p->ev[1], p->rstream));
     if ((rc = run_solver(p))) return rc;
     HIPCK(hipEventRecord(p->ev[2], p->stream));
     HIPCK(hipMemcpyAsync(p->h_ws, p->d.ws, sizeof(WorldState) * W, hipMemcpyDeviceToHost, p->stream));
@@ -1126,6 +1123,8 @@ int armour_get_reach_dump(armour_planner* p, double* dump, int capacity) {
     DeviceScope device_scope(p);
     if (!p) return fail(ARMOUR_E_ARG, "null planner");
     if (!p->d_dump) return fail(ARMOUR_E_STATE, "op dump is off (set ARMOUR_DUMP_OPS before armour_create)");
+    if (!p->lane_engine && p->has_lane)
+        return fail(ARMOUR_E_STATE, "the op dump follows the bundle engine, and the last batch ran on the per-job engine");
     if (dump && capacity >= p->nops) {
         if (p->lane_engine) {
             // [nops][DUMP_W][64] of bundle 0: lane ARMOUR_DUMP_LANE (default 0) = job of that index
@@ -1186,8 +1185,7 @@ int armour_get_reach_occupancy(armour_planner* p, long long* used, long long* ca
     if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
     if (!p->lane_engine || !p->d_occ)
         return fail(ARMOUR_E_STATE, "occupancy is recorded by the bundle engine only (this batch ran on the per-job engine)");
-    unsigned long long o[8] = {0};
-    HIPCK(hipMemcpy(o, p->d_occ, sizeof(o), hipMemcpyDeviceToHost));
+    const unsigned long long* o = p->h_occ;  // the first launch's maxima (a retry's 4x buffers excluded)
     const long long u[ARMOUR_OCC_COUNT] = {(long long)o[0], (long long)o[1], (long long)o[2], (long long)o[3],
                                            (long long)o[4], p->last_retried, p->last_failed};
     const long long c[ARMOUR_OCC_COUNT] = {p->la.hcap, p->la.ccap, std::min<long long>(p->la.gcap, (1 << 16) - 1),

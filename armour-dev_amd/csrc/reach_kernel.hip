@@ -23,9 +23,51 @@ constexpr int STAGE_DOUBLES = REACH_CFG_STAGE;
 constexpr int REACH_WG_PER_CU = REACH_CFG_WG_PER_CU;
 constexpr int POOL_DOUBLES = 1024;   // handle payloads (ProgramBuilder::slot_offsets)
 
-// JRS scalars of every (world, interval, joint) (KPR/Trajectory.cu:63-254), one thread each
+// The reach phase's counters: the algorithmic byte count, the capacity maxima occ[8] (arena
+// hashes, arena rows, operator terms, link / torque k-only monomials) and the per-world error
+// flags. jrs_kernel zeroes them; the reach kernel's last workgroup publishes them in mapped host
+// memory (hsum[0] bytes, hsum[1..8] occ, hsum[RSUM_ERR + w] world w's flags). So the host reads
+// them after one event wait, and no fill or copy runs on the reach stream: under concurrent
+// planners such a blit kernel would wait for CUs another planner's persistent reach kernel holds.
+constexpr int RSUM_ERR = 9;
+struct ReachCounters {
+    unsigned long long* bytes;  // [1]
+    unsigned long long* occ;    // [8]
+    unsigned* done;             // [1] workgroups finished (the last one resets it to 0)
+    long long* hsum;            // mapped host [RSUM_ERR + W]
+};
+
+__device__ inline void zero_counters(const ReachCounters& c, int* err, int W) {
+    if (blockIdx.x != 0) return;
+    for (int k = threadIdx.x; k < W; k += blockDim.x) err[k] = 0;
+    if (threadIdx.x < 8) c.occ[threadIdx.x] = 0;
+    if (threadIdx.x == 0) *c.bytes = 0;
+}
+
+// after a workgroup's last job: the last workgroup of the grid copies the counters out (reads
+// through device-scope atomics, so every other workgroup's updates are seen)
+__device__ inline void publish_counters(const ReachCounters& c, int* err, int W, int* last) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        *last = atomicAdd(c.done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!*last) return;
+    __threadfence();
+    for (int k = threadIdx.x; k < W; k += blockDim.x) c.hsum[RSUM_ERR + k] = atomicOr(&err[k], 0);
+    if (threadIdx.x < 8) c.hsum[1 + threadIdx.x] = (long long)atomicMax(&c.occ[threadIdx.x], 0ull);
+    if (threadIdx.x == 0) {
+        c.hsum[0] = (long long)atomicAdd(c.bytes, 0ull);
+        atomicExch(c.done, 0u);
+    }
+}
+
+// JRS scalars of every (world, interval, joint) (KPR/Trajectory.cu:63-254), one thread each;
+// block 0 also zeroes the reach phase's counters
 __global__ void jrs_kernel(const RobotParams* __restrict__ rpp, int W, int T, const double* q0, const double* qd0,
-                           const double* qdd0, JrsJoint* out) {
+                           const double* qdd0, JrsJoint* out, ReachCounters rc, int* err) {
+    zero_counters(rc, err, W);
     const long n = (long)W * T * NF;
     for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
         const int i = (int)(idx % NF);
@@ -39,7 +81,9 @@ __global__ void jrs_kernel(const RobotParams* __restrict__ rpp, int W, int T, co
 // relative joint angle rotated by q0, as the JRS scalars the reach program's MAKEROT reads (the
 // k-generator and the radius of the cos / sin 1-D PZs; radius x 5 as :43, :56). tables:
 // [W][NF][6][T] = c_cos, g_cos, r_cos, c_sin, g_sin, r_sin (armtd_main.cu:70-90)
-__global__ void jrs_armtd_kernel(int W, int T, const double* q0, const double* tables, JrsJoint* out) {
+__global__ void jrs_armtd_kernel(int W, int T, const double* q0, const double* tables, JrsJoint* out, ReachCounters rc,
+                                 int* err) {
+    zero_counters(rc, err, W);
     const long n = (long)W * T * NF;
     for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
         const int i = (int)(idx % NF);
@@ -79,6 +123,8 @@ struct ReachArgs {
     int gcap;
     double* gout;        // [grid][gcap * 9]
     unsigned long long* bytes;  // algorithmic monomial bytes of all jobs (one atomic per job)
+    ReachCounters rc;           // rc.occ[3] / [4]: largest link / torque k-only monomial counts
+    int ntq;                    // torque PZs per job (NF; the ARMTD program has none)
     unsigned long long* prof;   // optional per-op [cycles, terms] (null: off)
     int mode;                   // engine diagnostics (Ctx::mode)
     unsigned long long* phase;  // optional phase cycle totals [16] (null: off; exclusive with prof)
@@ -101,6 +147,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREA
     __shared__ double scratch[2 * NF];
     __shared__ double q0s[NF], qd0s[NF], qdd0s[NF];
     __shared__ unsigned long long phase_acc[16];
+    __shared__ int last;
 
     const RobotParams& rp = *rpp;
     Ctx x;
@@ -149,6 +196,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREA
         if (threadIdx.x == 0) {
             if (err) atomicOr(&out.err[w], err);
             atomicAdd(a.bytes, (unsigned long long)arena.bytes);
+            // this job's largest kept monomial counts (written by this thread in t0_emit_*), which
+            // size the evaluation kernels (planner.hip eval_small_fits)
+            int lm = 0, um = 0;
+            for (int l = 0; l < out.NJ; l++) lm = max(lm, out.link_cnt[job * out.NJ + l]);
+            for (int i = 0; i < a.ntq; i++) um = max(um, out.tq_cnt[job * NF + i]);
+            atomicMax(&a.rc.occ[3], (unsigned long long)lm);
+            atomicMax(&a.rc.occ[4], (unsigned long long)um);
         }
         if (a.phase && threadIdx.x < 16) {
             atomicAdd(&a.phase[threadIdx.x], phase_acc[threadIdx.x]);
@@ -156,6 +210,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREA
         }
         __syncthreads();
     }
+    publish_counters(a.rc, out.err, a.W, &last);
 }
 
 }  // namespace armour
