@@ -16,11 +16,25 @@
 // Buffer directory: argv[1], else $ARMOUR_BUFFER_DIR, else the build-time ARMOUR_BUFFER_PATH
 // (the reference bakes it into BufferPath.h), else <directory of this executable>/buffer/.
 // Time steps: $ARMOUR_NUM_TIME_STEPS, default 128 (NUM_TIME_STEPS, KPR/Parameters.h:17).
+//
+// Served mode ("optional persistent daemon keeps GPU context warm"). MATLAB starts a
+// new armour_main for every replan (uarmtd_planner.m:200); process start, HIP initialisation and
+// the planner's allocations are ~97 % of such a run. `armour_main --serve [buffer]` creates the
+// planner once (max_obstacles = MAX_OBSTACLE_NUM) and listens on <buffer>/armour.sock (or
+// $ARMOUR_SERVE_SOCKET). A plain `armour_main` first tries that socket: when a server answers, it
+// sends its buffer directory, the server plans that directory's armour.in and writes the same five
+// files, and the client exits with the server's status. Otherwise it plans in-process. The HIP
+// library is loaded with dlopen only on the in-process and server paths, so a served client never
+// maps the HIP runtime.
+#include <dlfcn.h>
+#include <signal.h>
+#include <sys/socket.h>
+#include <sys/un.h>
 #include <unistd.h>
 
-#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <iomanip>
 #include <iostream>
@@ -34,22 +48,29 @@ namespace {
 constexpr int NF = ARMOUR_NUM_FACTORS;
 constexpr int MAX_OBSTACLES = 40;  // MAX_OBSTACLE_NUM (KPR/Parameters.h:26)
 
-std::string buffer_dir(int argc, char** argv) {
+std::string exe_dir() {
+    char buf[4096];
+    const ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+    const std::string exe = n > 0 ? std::string(buf, (size_t)n) : std::string("./armour_main");
+    return exe.substr(0, exe.find_last_of('/') + 1);
+}
+
+std::string buffer_dir(const char* arg) {
     std::string d;
-    if (argc > 1) d = argv[1];
+    if (arg) d = arg;
     else if (const char* e = std::getenv("ARMOUR_BUFFER_DIR")) d = e;
 #ifdef ARMOUR_BUFFER_PATH
     else d = ARMOUR_BUFFER_PATH;
 #else
-    else {
-        char buf[4096];
-        const ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
-        std::string exe = n > 0 ? std::string(buf, (size_t)n) : std::string("./armour_main");
-        d = exe.substr(0, exe.find_last_of('/') + 1) + "buffer";
-    }
+    else d = exe_dir() + "buffer";
 #endif
     if (!d.empty() && d.back() != '/') d += '/';
     return d;
+}
+
+std::string socket_path(const std::string& dir) {
+    if (const char* e = std::getenv("ARMOUR_SERVE_SOCKET")) return e;
+    return dir + "armour.sock";
 }
 
 int fail_out(const std::string& out1, const char* msg) {
@@ -59,10 +80,58 @@ int fail_out(const std::string& out1, const char* msg) {
     return 1;
 }
 
-}  // namespace
+// the C ABI of libarmour_hip.so, resolved at run time
+struct Lib {
+    decltype(&armour_create) create;
+    decltype(&armour_destroy) destroy;
+    decltype(&armour_last_error) last_error;
+    decltype(&armour_plan_batch) plan_batch;
+    decltype(&armour_num_joints) num_joints;
+    decltype(&armour_num_constraints) num_constraints;
+    decltype(&armour_get_link_centers) link_centers;
+    decltype(&armour_get_link_generators) link_generators;
+    decltype(&armour_get_torque_radius) torque_radius;
+    decltype(&armour_get_constraints) constraints;
+    decltype(&armour_get_joint_bounds) joint_bounds;
 
-int main(int argc, char** argv) {
-    const std::string dir = buffer_dir(argc, argv);
+    bool load(std::string& why) {
+        const char* env = std::getenv("ARMOUR_LIB");
+        const std::string path = env ? env : exe_dir() + "libarmour_hip.so";
+        void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            why = dlerror();
+            return false;
+        }
+        bool ok = true;
+        auto sym = [&](auto& f, const char* name) {
+            f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+            ok = ok && f;
+        };
+        sym(create, "armour_create");
+        sym(destroy, "armour_destroy");
+        sym(last_error, "armour_last_error");
+        sym(plan_batch, "armour_plan_batch");
+        sym(num_joints, "armour_num_joints");
+        sym(num_constraints, "armour_num_constraints");
+        sym(link_centers, "armour_get_link_centers");
+        sym(link_generators, "armour_get_link_generators");
+        sym(torque_radius, "armour_get_torque_radius");
+        sym(constraints, "armour_get_constraints");
+        sym(joint_bounds, "armour_get_joint_bounds");
+        if (!ok) why = "libarmour_hip.so lacks an armour_* symbol";
+        return ok;
+    }
+};
+
+int time_steps() {
+    const char* e = std::getenv("ARMOUR_NUM_TIME_STEPS");
+    return e ? std::atoi(e) : 128;
+}
+
+// One replan of the buffer directory `dir`: read armour.in, plan, write the five outputs. With
+// `served` a planner of the right horizon is given (capacity MAX_OBSTACLE_NUM); otherwise one is
+// created for this input and destroyed.
+int plan_dir(const Lib& L, armour_planner* served, const std::string& dir) {
     const std::string in = dir + "armour.in", out1 = dir + "armour.out";
     // a fresh armour.out on every run, as the reference (armour_main.cu:36-37)
     { std::ofstream o(out1); }
@@ -81,11 +150,18 @@ int main(int argc, char** argv) {
         for (double& v : obs) is >> v;
     }
 
-    int T = 128;
-    if (const char* e = std::getenv("ARMOUR_NUM_TIME_STEPS")) T = std::atoi(e);
-    armour_config cfg{0, T, O, 1, 0, 0};
-    armour_planner* p = armour_create(&cfg);
-    if (!p) return fail_out(out1, armour_last_error());
+    const int T = time_steps();
+    armour_planner* p = served;
+    if (!p) {
+        armour_config cfg{0, T, O, 1, 0, 0};
+        p = L.create(&cfg);
+        if (!p) return fail_out(out1, L.last_error());
+    }
+    struct Owned {
+        const Lib& L;
+        armour_planner* p;
+        ~Owned() { if (p) L.destroy(p); }
+    } owned{L, served ? nullptr : p};
 
     armour_world w;
     for (int i = 0; i < NF; i++) { w.q0[i] = q0[i]; w.qd0[i] = qd0[i]; w.qdd0[i] = qdd0[i]; w.q_des[i] = qdes[i]; }
@@ -94,31 +170,22 @@ int main(int argc, char** argv) {
 
     armour_result r;
     armour_timing tm;
-    if (armour_plan_batch(p, 1, &w, &r, &tm) != 0) {
-        const int rc = fail_out(out1, armour_last_error());
-        armour_destroy(p);
-        return rc;
-    }
+    if (L.plan_batch(p, 1, &w, &r, &tm) != 0) return fail_out(out1, L.last_error());
     std::cout << "        HIP: reachable sets " << tm.reach_ms << " ms, solver " << tm.nlp_ms << " ms, "
               << (r.feasible ? "found a feasible solution" : "no feasible solution") << std::endl;
     // a reach set over the library's capacity is not planned: reported as no feasible solution
     // (-1, MATLAB keeps its braking trajectory), with the reason on stderr
-    if (r.error) std::fprintf(stderr, "        armour_main: %s\n", armour_last_error());
+    if (r.error) std::fprintf(stderr, "        armour_main: %s\n", L.last_error());
 
-    const int NJ = armour_num_joints(p);
-    const int m = armour_num_constraints(p, O);
+    const int NJ = L.num_joints(p);
+    const int m = L.num_constraints(p, O);
     std::vector<double> centers((size_t)T * NJ * 3), gens((size_t)T * NJ * 18), rad((size_t)T * NF), g(m), bounds(4 * NF);
-    int rc = armour_get_link_centers(p, 0, centers.data());
-    rc = rc ? rc : armour_get_link_generators(p, 0, gens.data());
-    rc = rc ? rc : armour_get_torque_radius(p, 0, rad.data());
-    rc = rc ? rc : armour_get_constraints(p, 0, g.data());
-    rc = rc ? rc : armour_get_joint_bounds(p, bounds.data());
-    if (rc) {
-        const int e = fail_out(out1, armour_last_error());
-        armour_destroy(p);
-        return e;
-    }
-    armour_destroy(p);
+    int rc = L.link_centers(p, 0, centers.data());
+    rc = rc ? rc : L.link_generators(p, 0, gens.data());
+    rc = rc ? rc : L.torque_radius(p, 0, rad.data());
+    rc = rc ? rc : L.constraints(p, 0, g.data());
+    rc = rc ? rc : L.joint_bounds(p, bounds.data());
+    if (rc) return fail_out(out1, L.last_error());
 
     {
         std::ofstream o(out1);
@@ -163,4 +230,94 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 4 * NF; i++) o << bounds[i] << '\n';
     }
     return 0;
+}
+
+bool fill_addr(sockaddr_un& a, const std::string& path) {
+    std::memset(&a, 0, sizeof(a));
+    a.sun_family = AF_UNIX;
+    if (path.size() >= sizeof(a.sun_path)) return false;
+    std::memcpy(a.sun_path, path.c_str(), path.size());
+    return true;
+}
+
+// client: -1 when no server answers (plan in-process), else the server's exit status
+int try_served(const std::string& dir) {
+    sockaddr_un a;
+    if (!fill_addr(a, socket_path(dir))) return -1;
+    const int fd = socket(AF_UNIX, SOCK_STREAM, 0);
+    if (fd < 0) return -1;
+    if (connect(fd, (sockaddr*)&a, sizeof(a)) != 0) {
+        close(fd);
+        return -1;
+    }
+    const std::string req = dir + "\n";
+    unsigned char rc = 1;
+    const bool ok = write(fd, req.data(), req.size()) == (ssize_t)req.size() && read(fd, &rc, 1) == 1;
+    close(fd);
+    return ok ? (int)rc : 1;
+}
+
+std::string g_sock;
+void on_signal(int) {
+    if (!g_sock.empty()) unlink(g_sock.c_str());
+    _exit(0);
+}
+
+int serve(const Lib& L, const std::string& dir) {
+    const int T = time_steps();
+    armour_config cfg{0, T, MAX_OBSTACLES, 1, 0, 0};
+    armour_planner* p = L.create(&cfg);
+    if (!p) {
+        std::fprintf(stderr, "armour_main --serve: %s\n", L.last_error());
+        return 1;
+    }
+    g_sock = socket_path(dir);
+    sockaddr_un a;
+    if (!fill_addr(a, g_sock)) {
+        std::fprintf(stderr, "armour_main --serve: socket path too long: %s\n", g_sock.c_str());
+        return 1;
+    }
+    const int fd = socket(AF_UNIX, SOCK_STREAM, 0);
+    unlink(g_sock.c_str());
+    if (fd < 0 || bind(fd, (sockaddr*)&a, sizeof(a)) != 0 || listen(fd, 16) != 0) {
+        std::perror("armour_main --serve: socket");
+        return 1;
+    }
+    signal(SIGTERM, on_signal);
+    signal(SIGINT, on_signal);
+    signal(SIGPIPE, SIG_IGN);
+    std::fprintf(stderr, "armour_main: serving %s (T = %d)\n", g_sock.c_str(), T);
+    for (;;) {
+        const int c = accept(fd, nullptr, nullptr);
+        if (c < 0) continue;
+        std::string req;
+        char buf[512];
+        ssize_t n;
+        while (req.find('\n') == std::string::npos && (n = read(c, buf, sizeof(buf))) > 0) req.append(buf, (size_t)n);
+        const size_t e = req.find('\n');
+        unsigned char rc = 1;
+        if (e != std::string::npos) {
+            std::string d = req.substr(0, e);
+            if (!d.empty() && d.back() != '/') d += '/';
+            rc = (unsigned char)plan_dir(L, p, d);
+        }
+        (void)!write(c, &rc, 1);
+        close(c);
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const bool served = argc > 1 && std::strcmp(argv[1], "--serve") == 0;
+    const char* arg = served ? (argc > 2 ? argv[2] : nullptr) : (argc > 1 ? argv[1] : nullptr);
+    const std::string dir = buffer_dir(arg);
+    if (!served && !std::getenv("ARMOUR_NO_SERVE")) {
+        const int rc = try_served(dir);
+        if (rc >= 0) return rc;
+    }
+    Lib L;
+    std::string why;
+    if (!L.load(why)) return fail_out(dir + "armour.out", why.c_str());
+    return served ? serve(L, dir) : plan_dir(L, nullptr, dir);
 }

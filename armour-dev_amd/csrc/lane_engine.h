@@ -119,6 +119,21 @@ DI uint32_t uu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((in
 DI double ud(double v) { return __builtin_bit_cast(double, bcast0(__builtin_bit_cast(long, v))); }
 template <class T>
 DI T* up(T* p) { return (T*)(uintptr_t)bcast0((long)(uintptr_t)p); }
+// a wave-uniform value the optimiser cannot see through (readfirstlane, then an empty asm on the
+// scalar register)
+DI int opaque(int v) {
+    int r = __builtin_amdgcn_readfirstlane(v);
+    __asm__ volatile("" : "+s"(r));
+    return r;
+}
+DI long opaque(long v) {
+    long r = bcast0(v);
+    __asm__ volatile("" : "+s"(r));
+    return r;
+}
+DI double opaque(double v) { return __builtin_bit_cast(double, opaque(__builtin_bit_cast(long, v))); }
+template <class T>
+DI const T* opaque(const T* p) { return (const T*)(uintptr_t)opaque((long)(uintptr_t)p); }
 
 // per-lane header rows
 DI double& P(const LCtx& x, int row) { return x.pool[(long)row * LG + x.lane]; }
@@ -583,22 +598,23 @@ struct GMul {
     double Ac[NA], Bc[NB];
     DI void ra(int k, double* a, int lane) const { rows<NA>(ca, k, a, lane); }
     DI void rb(int k, double* b, int lane) const { rows<NB>(cb, k, b, lane); }
+    // Branch-free (p is wave-uniform): both factors' rows are always loaded, from clamped monomial
+    // indices (a handle without monomials reads a safe row, gen_mul), and the centre is selected in
+    // for T1 / T2 terms. A load inside a branch makes the compiler wait for it where the branches
+    // meet, which serialised the memory latencies of a round's groups.
     DI void factors(int p, double* a, double* b, int lane) const {
-        if (p < na) {
-            ra(p, a, lane);
+        const bool ta = p < na, tb = !ta && p < na + nb;
+        const int q = p - na - nb;
+        const int iq = nb == 1 ? q : (int)__umulhi((uint32_t)(q > 0 ? q : 0), nbm);
+        const int i = ta ? p : (tb ? 0 : iq);
+        const int j = tb ? p - na : (ta ? 0 : q - iq * nb);
+        double la[NA], lb[NB];
+        ra(i, la, lane);
+        rb(j, lb, lane);
 #pragma unroll
-            for (int e = 0; e < NB; e++) b[e] = Bc[e];
-        } else if (p < na + nb) {
+        for (int e = 0; e < NA; e++) a[e] = tb ? Ac[e] : la[e];
 #pragma unroll
-            for (int e = 0; e < NA; e++) a[e] = Ac[e];
-            rb(p - na, b, lane);
-        } else {
-            const int q = p - na - nb;
-            const int i = nb == 1 ? q : (int)__umulhi((uint32_t)q, nbm);
-            const int j = q - i * nb;
-            ra(i, a, lane);
-            rb(j, b, lane);
-        }
+        for (int e = 0; e < NB; e++) b[e] = ta ? Bc[e] : lb[e];
     }
     DI void term(int p, double* v, int lane) const {
         double a[NA], b[NB];
@@ -620,10 +636,12 @@ struct GMul {
 template <int NA, int NB>
 DI GMul<NA, NB> gen_mul(const LCtx& x, const LH& A, const LH& B) {
     GMul<NA, NB> G;
-    G.ca = up(x.A->c) + bcast0(A.coff) * LG;
-    G.cb = up(x.A->c) + bcast0(B.coff) * LG;
     G.na = ui(A.cnt);
     G.nb = ui(B.cnt);
+    // an operand without monomials (a constant matrix) points at the arena's first rows, so the
+    // branch-free factors() never reads past an allocation
+    G.ca = up(x.A->c) + (G.na > 0 ? bcast0(A.coff) : 0) * LG;
+    G.cb = up(x.A->c) + (G.nb > 0 ? bcast0(B.coff) : 0) * LG;
     G.nbm = G.nb > 1 ? 0xFFFFFFFFu / (uint32_t)G.nb + 1u : 0u;
 #pragma unroll
     for (int e = 0; e < NA; e++) G.Ac[e] = cen(x, A, e);
@@ -661,22 +679,33 @@ struct GCat {
     int c0, c1;
     DI void term(int p, double* v, int lane) const {
         const int s = p < c0 ? 0 : (p < c0 + c1 ? 1 : 2);
-        const D& d = s == 0 ? d0 : (s == 1 ? d1 : d2);
+        // Field-by-field value selects (all wave-uniform, so scalar registers). A reference to the
+        // selected descriptor is a pointer select: the compiler then keeps d0..d2 in scratch and
+        // every term pays a chain of dependent scratch loads (descriptor, row, flags, scale).
+        // (opaque(): the optimiser would fold a select of two field loads back into one load from
+        // a selected address)
+        const double* c = s == 0 ? opaque(d0.c) : (s == 1 ? opaque(d1.c) : opaque(d2.c));
+        const int stride = s == 0 ? opaque(d0.stride) : (s == 1 ? opaque(d1.stride) : opaque(d2.stride));
+        const int comp = s == 0 ? opaque(d0.comp) : (s == 1 ? opaque(d1.comp) : opaque(d2.comp));
+        const int one = s == 0 ? opaque(d0.one) : (s == 1 ? opaque(d1.one) : opaque(d2.one));
+        const int place = s == 0 ? opaque(d0.place) : (s == 1 ? opaque(d1.place) : opaque(d2.place));
+        const int neg = s == 0 ? opaque(d0.neg) : (s == 1 ? opaque(d1.neg) : opaque(d2.neg));
+        const int scaled = s == 0 ? opaque(d0.scaled) : (s == 1 ? opaque(d1.scaled) : opaque(d2.scaled));
+        const double scale = s == 0 ? opaque(d0.scale) : (s == 1 ? opaque(d1.scale) : opaque(d2.scale));
         const int k = s == 0 ? p : (s == 1 ? p - c0 : p - c0 - c1);
-        const double* base = d.c + (long)k * d.stride * LG + lane;
-        if (d.one) {
-            double x0 = base[(long)(d.comp >= 0 ? d.comp : 0) * LG];
-            if (d.scaled) x0 = d.scale * x0;
-            if (d.neg) x0 = -x0;
+        const double* base = c + (long)k * stride * LG + lane;
+        // branch-free: N loads either way (a 1x1 source reads its one element N times, the same
+        // 512-byte row), then the same arithmetic as the per-element form
+        const int e1 = comp >= 0 ? comp : 0;
+        double xs[N];
 #pragma unroll
-            for (int e = 0; e < N; e++) v[e] = (e == d.place) ? x0 : 0.0;
-        } else {
+        for (int e = 0; e < N; e++) xs[e] = base[(long)(one ? e1 : e) * LG];
 #pragma unroll
-            for (int e = 0; e < N; e++) {
-                double x0 = base[(long)e * LG];
-                if (d.scaled) x0 = d.scale * x0;
-                v[e] = d.neg ? -x0 : x0;
-            }
+        for (int e = 0; e < N; e++) {
+            double x0 = xs[e];
+            if (scaled) x0 = scale * x0;
+            x0 = neg ? -x0 : x0;
+            v[e] = one ? ((e == place) ? x0 : 0.0) : x0;
         }
     }
 };
@@ -800,26 +829,44 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
     }
     for (int r0 = 0, par = 0; r0 < NG; r0 += RG, par ^= 1) {
         RSTAMP(7)
+        // every index load of the round is issued before the first is used (clamped, no branches),
+        // then every group's first-member loads, so the round costs one latency per phase
         int lo[U], sz[U];
         int maxsz = 0;
+        {
+            int l0[U], h0[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int g = r0 + x.wave * U + u;
-            const bool in = g < NG;
-            lo[u] = in ? ui(gp[g]) : 0;
-            sz[u] = in ? ui(gp[g + 1]) - lo[u] : 0;
-            maxsz = sz[u] > maxsz ? sz[u] : maxsz;
+            for (int u = 0; u < U; u++) {
+                const int g = min(r0 + x.wave * U + u, NG);
+                l0[u] = gp[g];
+                h0[u] = gp[min(g + 1, NG)];
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const bool in = r0 + x.wave * U + u < NG;
+                lo[u] = in ? ui(l0[u]) : 0;
+                sz[u] = in ? ui(h0[u]) - lo[u] : 0;
+                maxsz = sz[u] > maxsz ? sz[u] : maxsz;
+            }
         }
         RSTAMP(0)
         sub[5] += 1;
         sub[6] += maxsz;
         double acc[U][NV];
+        {
+            int p0[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) G.term(ui((int)ki[lo[u]]), acc[u], x.lane);
+            for (int u = 0; u < U; u++) p0[u] = (int)ki[lo[u]];
+#pragma unroll
+            for (int u = 0; u < U; u++) G.term(ui(p0[u]), acc[u], x.lane);
+        }
         for (int r = 1; r < maxsz; r++) {
             double tmp[U][NV];
+            int pr[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) G.term(ui((int)ki[lo[u] + (r < sz[u] ? r : 0)]), tmp[u], x.lane);
+            for (int u = 0; u < U; u++) pr[u] = (int)ki[lo[u] + (r < sz[u] ? r : 0)];
+#pragma unroll
+            for (int u = 0; u < U; u++) G.term(ui(pr[u]), tmp[u], x.lane);
 #pragma unroll
             for (int u = 0; u < U; u++)
                 if (r < sz[u])

@@ -25,6 +25,10 @@ struct IpmOpts {
     double kappa_sigma = 1e10;
     double s_max = 100.0;
     double inf_bound = 1e19;
+    // barrier strategy: 0 monotone (default); 1 adaptive (ARMOUR_MU_STRATEGY=adaptive: the
+    // reference's IPOPT_MU_STRATEGY, KPR/Parameters.h:57, with the LOQO mu oracle and the kkt-error
+    // globalisation, as oracle/src/ipm.cpp; DESIGN.md §5 for why it is not the default)
+    int mu_strategy = 0;
 };
 
 struct WorldState {
@@ -43,6 +47,10 @@ struct WorldState {
     int ftype;
     int first_update, nfail, iter, nevals, ls;
     int spec_k;        // trial of the speculative round that ended the line search (-1: none)
+    // adaptive barrier: free (oracle) mode, and the KKT errors the globalisation compares against
+    // (free mode: the last <= 4; fixed mode: the one at the switch)
+    int free_mode, nref;
+    double kkt_ref[4];
 };
 
 struct NlpDev {

@@ -1329,6 +1329,8 @@ __global__ __launch_bounds__(64) void ipm_world_init(NlpDev d) {
     S.iter = 0;
     S.nevals = 1;
     S.kkt = 0;
+    S.free_mode = d.opt.mu_strategy == 1 ? 1 : 0;
+    S.nref = 0;
 }
 
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
@@ -1365,12 +1367,14 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
 struct AAcc {
     double rdp[NF], M[28], u1[NF], u2[NF];
     double inf_p, compl0, cm, sumz;
+    double sumc, minc;  // sum and minimum of s z over the finite sides (the adaptive barrier's oracle)
     __device__ void zero() {
 #pragma unroll
         for (int j = 0; j < NF; j++) { rdp[j] = 0; u1[j] = 0; u2[j] = 0; }
 #pragma unroll
         for (int k = 0; k < 28; k++) M[k] = 0;
         inf_p = 0; compl0 = 0; cm = 0; sumz = 0;
+        sumc = 0; minc = 1e300;
     }
 };
 __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, long i, double v, const double* a, double L,
@@ -1385,6 +1389,8 @@ __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, lon
         c.compl0 = fmax(c.compl0, s * z);
         c.cm = fmax(c.cm, fabs(s * z - mu));
         c.sumz += z;
+        c.sumc += s * z;
+        c.minc = fmin(c.minc, s * z);
         const double sg = z / s;
         sig += sg;
         c1 += 1.0 / s;
@@ -1399,6 +1405,8 @@ __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, lon
         c.compl0 = fmax(c.compl0, s * z);
         c.cm = fmax(c.cm, fabs(s * z - mu));
         c.sumz += z;
+        c.sumc += s * z;
+        c.minc = fmin(c.minc, s * z);
         const double sg = z / s;
         sig += sg;
         c1 -= 1.0 / s;
@@ -1414,17 +1422,20 @@ __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, lon
         for (int q = p; q < NF; q++) c.M[k++] += sig * a[p] * a[q];
     }
 }
+constexpr int NA = 55;  // pass A's partial sums per row block (<= KA)
+static_assert(NA <= KA, "pass A partials fit the partial slots");
 __device__ inline void reduce_A(const NlpDev& d, int w, AAcc& c, double* lds) {
     double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
-    double v[53];
-    int kinds[53];
+    double v[NA];
+    int kinds[NA];
 #pragma unroll
     for (int j = 0; j < NF; j++) { v[j] = c.rdp[j]; v[39 + j] = c.u1[j]; v[46 + j] = c.u2[j]; }
     v[7] = c.inf_p; v[8] = c.compl0; v[9] = c.cm; v[10] = c.sumz;
 #pragma unroll
     for (int k = 0; k < 28; k++) v[11 + k] = c.M[k];
+    v[53] = c.sumc; v[54] = c.minc;
 #pragma unroll
-    for (int k = 0; k < 53; k++) kinds[k] = (k >= 7 && k <= 9) ? 1 : 0;
+    for (int k = 0; k < NA; k++) kinds[k] = (k >= 7 && k <= 9) ? 1 : k == 54 ? 2 : 0;
     block_reduce_n(v, kinds, lds, out);
 }
 // pass D's row update (accept the trial: slacks, multipliers) and the BFGS ingredient sum w a
@@ -1454,7 +1465,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    __shared__ double lds[(ROW_THREADS / 64) * NA];
     AAcc c;
     c.zero();
     const double mu = S.mu;
@@ -1478,7 +1489,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    __shared__ double lds[(ROW_THREADS / 64) * NA];
     const double mu = S.mu, ad = S.ad, alpha = S.alpha;
     double wn[NF];
 #pragma unroll
@@ -1579,10 +1590,10 @@ __device__ inline void world_A_body(const NlpDev& d, int w, int nside) {
         if (threadIdx.x == 0) S.status = 2;
         return;
     }
-    double P[53], init[53];
-    int op[53];
+    double P[NA], init[NA];
+    int op[NA];
 #pragma unroll
-    for (int k = 0; k < 53; k++) { init[k] = 0; op[k] = (k >= 7 && k <= 9) ? 1 : 0; }
+    for (int k = 0; k < NA; k++) { init[k] = k == 54 ? 1e300 : 0; op[k] = (k >= 7 && k <= 9) ? 1 : k == 54 ? 2 : 0; }
     world_partials(d, w, init, op, P);
     if (threadIdx.x != 0) return;
     const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
@@ -1593,7 +1604,42 @@ __device__ inline void world_A_body(const NlpDev& d, int w, int nside) {
     S.kkt = E0;
     if (E0 <= d.opt.tol) { S.status = 1; return; }
     const double Emu = fmax(fmax(inf_d / sd, P[7]), P[9] / sd);
-    if (Emu <= d.opt.kappa_eps * S.mu && S.mu > d.opt.tol / 10) {
+    if (d.opt.mu_strategy == 1) {
+        // adaptive barrier (oracle/src/ipm.cpp, same order of decisions): free mode takes mu from
+        // the LOQO oracle; the kkt-error globalisation switches to fixed (monotone) mode when E0 has
+        // not fallen below 0.9999 x the largest of the last four, back once below the switch value
+        const double avg = P[53] / (double)(nside > 0 ? nside : 1), mn = P[54];
+        bool progress = S.nref < 4;
+        if (!progress) {
+            double mx = 0;
+            for (int q = 0; q < 4; q++) mx = fmax(mx, S.kkt_ref[q]);
+            progress = E0 <= 0.9999 * mx;
+        }
+        const double mu_old = S.mu;
+        if (S.free_mode && !progress) {
+            S.free_mode = 0;
+            S.mu = fmax(1e-11, 0.8 * avg);
+            S.kkt_ref[0] = E0;
+            S.nref = 1;
+        } else if (!S.free_mode && progress && S.nref >= 1 && E0 <= 0.9999 * S.kkt_ref[S.nref - 1]) {
+            S.free_mode = 1;
+            S.nref = 0;
+        }
+        if (S.free_mode) {
+            if (S.nref == 4) {
+                for (int q = 0; q < 3; q++) S.kkt_ref[q] = S.kkt_ref[q + 1];
+                S.kkt_ref[3] = E0;
+            } else {
+                S.kkt_ref[S.nref++] = E0;
+            }
+            const double xi = mn / avg;
+            const double sg = 0.1 * pow(fmin(0.05 * (1 - xi) / xi, 2.0), 3);
+            S.mu = fmax(1e-11, fmin(sg * avg, 1e5));
+        } else if (Emu <= d.opt.kappa_eps * S.mu && S.mu > d.opt.tol / 10) {
+            S.mu = fmax(d.opt.tol / 10, fmin(d.opt.kappa_mu * S.mu, pow(S.mu, d.opt.theta_mu)));
+        }
+        if (S.mu != mu_old) S.nfilt = 0;
+    } else if (Emu <= d.opt.kappa_eps * S.mu && S.mu > d.opt.tol / 10) {
         S.mu = fmax(d.opt.tol / 10, fmin(d.opt.kappa_mu * S.mu, pow(S.mu, d.opt.theta_mu)));
         S.nfilt = 0;
     }
@@ -1627,7 +1673,7 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    __shared__ double lds[(ROW_THREADS / 64) * NA];
     const double mu = S.mu;
     const double tau = fmax(d.opt.tau_min, 1.0 - mu);
     double ap = 1.0, ad = 1.0, rp1 = 0, bdir = 0, logs = 0, wa[NF], wb[NF];
@@ -1717,7 +1763,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
-    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    __shared__ double lds[(ROW_THREADS / 64) * NA];
     double logt = 0, rpt = 0;
     const long r0 = (long)blockIdx.x * d.chunk;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
@@ -1831,7 +1877,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
     const int w = d.wl[i];
     const WorldState& S = d.ws[w];
     if (!(S.status == 0 && S.searching)) return;
-    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    __shared__ double lds[(ROW_THREADS / 64) * NA];
     double alpha = S.alpha;
     for (int q = 0; q < k; q++) alpha *= 0.5;
     const double* G = d.gs + (long)blockIdx.y * d.m;
@@ -1899,7 +1945,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
-    __shared__ double lds[(ROW_THREADS / 64) * 53];
+    __shared__ double lds[(ROW_THREADS / 64) * NA];
     const double mu = S.mu, ad = S.ad, alpha = S.alpha;
     double wn[NF];
 #pragma unroll

@@ -362,6 +362,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     d.NJ = NJ;
     d.ro = ro;
     if (cfg->max_iter > 0) d.opt.max_iter = cfg->max_iter;
+    if (const char* ms = std::getenv("ARMOUR_MU_STRATEGY"))  // the reference's adaptive barrier (option)
+        d.opt.mu_strategy = std::strcmp(ms, "adaptive") == 0 ? 1 : 0;
     d.armtd = p->armtd ? 1 : 0;
     d.nt = p->armtd ? 0 : NF * T;
     d.krange = nullptr;

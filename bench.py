@@ -225,13 +225,18 @@ def main():
     if world_size != a.gpus and a.gpus > 1:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world_size}", file=sys.stderr)
     dist = None
+    # collective backend: "nccl" (= RCCL over xGMI, one rank per GPU); ARMOUR_DIST_BACKEND=gloo runs
+    # the same path with host-side collectives (tests/test_gpu_dist.py: two ranks sharing one GPU)
+    backend = os.environ.get("ARMOUR_DIST_BACKEND", "nccl")
+    coll_device = "cuda" if backend == "nccl" else None
     if world_size > 1:
         import torch
         import torch.distributed as dist_mod
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local_rank = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local_rank)
-        dist_mod.init_process_group("nccl", rank=rank, world_size=world_size)
+        dist_mod.init_process_group(backend, rank=rank, world_size=world_size)
         dist = dist_mod
 
     import armour_amd as A
@@ -294,7 +299,7 @@ def main():
         return [r for o in out for r in o[0]], [o[1] for o in out]
 
     def gather(res):
-        return D.gather(D.records(res), dist, device="cuda" if dist is not None else None,
+        return D.gather(D.records(res), dist, device=coll_device if dist is not None else None,
                         total=total_job if strong else None)
 
     def barrier():
@@ -323,7 +328,7 @@ def main():
     if dist is not None:
         import torch
 
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_device or "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     if rank != 0:

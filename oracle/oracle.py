@@ -49,6 +49,7 @@ def lib():
                                 ctypes.POINTER(ctypes.c_ulonglong), _dp, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.oracle_plan.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, ctypes.c_int]
+        L.oracle_plan_mu.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, ctypes.c_int, ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -154,11 +155,13 @@ class OraclePlanner:
         return dict(rows=r.value, cols=cl.value, center=c[:k], indep=ind[:k], hashes=hs[:n],
                     coeffs=co[:n, :k])
 
-    def plan(self, max_iter=0):
+    def plan(self, max_iter=0, mu_strategy=0):
+        """mu_strategy 0: monotone barrier (the build's solver); 1: adaptive (KPR/Parameters.h:57's
+        strategy, an option: DESIGN.md §5)"""
         k = np.zeros(7)
         g = np.zeros(self.m)
         stats = np.zeros(8)
-        feas = lib().oracle_plan(self.h, _ptr(k), _ptr(g), _ptr(stats), max_iter)
+        feas = lib().oracle_plan_mu(self.h, _ptr(k), _ptr(g), _ptr(stats), max_iter, mu_strategy)
         if feas < 0:
             raise RuntimeError("oracle plan failed")
         return dict(k_opt=k, feasible=bool(feas), g=g, reach_ms=stats[0], nlp_ms=stats[1],

@@ -230,7 +230,13 @@ int oracle_pz(void* h, int kind, int idx, double* center, double* indep, unsigne
 
 // full plan: reach + NLP + finalize. stats[0]=reach ms, [1]=nlp ms, [2]=iterations, [3]=evals,
 // [4]=solver status, [5]=objective/cost_scale, [6]=kkt error. Returns 1 feasible, 0 infeasible, -1 error.
+int oracle_plan_mu(void* h, double* k_opt, double* g_out, double* stats, int max_iter, int mu_strategy);
 int oracle_plan(void* h, double* k_opt, double* g_out, double* stats, int max_iter) {
+    return oracle_plan_mu(h, k_opt, g_out, stats, max_iter, 0);
+}
+
+// the same with the barrier strategy chosen (0 monotone, the default; 1 adaptive: DESIGN.md §5)
+int oracle_plan_mu(void* h, double* k_opt, double* g_out, double* stats, int max_iter, int mu_strategy) {
     Planner* P = static_cast<Planner*>(h);
     auto t0 = std::chrono::high_resolution_clock::now();
     try {
@@ -243,6 +249,7 @@ int oracle_plan(void* h, double* k_opt, double* g_out, double* stats, int max_it
     IpmOptions opt;
     opt.tol = P->tol;
     if (max_iter > 0) opt.max_iter = max_iter;
+    opt.mu_strategy = mu_strategy;
     double x[NF] = {0, 0, 0, 0, 0, 0, 0};  // NLPclass.cu:193-199
     std::vector<double> g(P->m());
     IpmResult r = ipm_solve(nlp, opt, x, g.data());

@@ -97,6 +97,14 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
     std::vector<double> filt_theta, filt_phi;
     double theta_max = -1, theta_min = -1;
     int nfail = 0;
+    // adaptive barrier (mu_strategy 1): free mode takes mu from the LOQO oracle every iteration;
+    // the kkt-error globalisation switches to monotone (fixed) mode when the KKT error has not
+    // fallen below 0.9999 x the largest of the last 4 reference values, and back to free mode once
+    // it has (Ipopt: adaptive_mu_globalization kkt-error, kkterror_red_iters 4, red_fact 0.9999,
+    // adaptive_mu_monotone_init_factor 0.8, mu_oracle loqo)
+    bool free_mode = opt.mu_strategy == 1;
+    std::vector<double> kkt_ref;
+    const double mu_min = 1e-11;
     IpmResult res{1, 0, 0, 0.0, 0.0};
     double a[NMAX], at[NMAX];
     int it;
@@ -134,19 +142,61 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
         const double E0 = std::max(std::max(inf_d / sd, inf_p), compl0 / sd);
         res.kkt_error = E0;
         if (E0 <= opt.tol) { res.status = 0; break; }
-        // 2. monotone barrier update (at most one decrease per iteration)
+        // 2. barrier update. Emu is the barrier problem's error at the iteration's starting mu.
+        double Emu;
         {
             double cm = 0;
             for (int r = 0; r < R; r++) {
                 if (hlo[r]) cm = std::max(cm, std::fabs(slo[r] * zlo[r] - mu));
                 if (hhi[r]) cm = std::max(cm, std::fabs(shi[r] * zhi[r] - mu));
             }
-            const double Emu = std::max(std::max(inf_d / sd, inf_p), cm / sd);
-            if (Emu <= opt.kappa_eps * mu && mu > opt.tol / 10) {
+            Emu = std::max(std::max(inf_d / sd, inf_p), cm / sd);
+        }
+        if (opt.mu_strategy == 1) {
+            // adaptive (Ipopt's mu_strategy "adaptive", KPR/Parameters.h:57): free mode takes mu
+            // from the LOQO oracle, sigma = 0.1 min(0.05 (1 - xi) / xi, 2)^3 with xi = min(s z) /
+            // avg(s z); the kkt-error globalisation switches to fixed (monotone) mode, from
+            // 0.8 x avg(s z), when E0 has not fallen below 0.9999 x the largest of the last four
+            // free-mode values, and back to free mode once E0 is below 0.9999 x its value at the switch
+            double sum = 0, mn = 1e300;
+            for (int r = 0; r < R; r++) {
+                if (hlo[r]) { const double c = slo[r] * zlo[r]; sum += c; mn = std::min(mn, c); }
+                if (hhi[r]) { const double c = shi[r] * zhi[r]; sum += c; mn = std::min(mn, c); }
+            }
+            const double avg = sum / std::max(1, nside);
+            bool progress = kkt_ref.size() < 4;
+            if (!progress) {
+                double mx = 0;
+                for (double v : kkt_ref) mx = std::max(mx, v);
+                progress = E0 <= 0.9999 * mx;
+            }
+            const double mu_old = mu;
+            if (free_mode && !progress) {
+                free_mode = false;
+                mu = std::max(mu_min, 0.8 * avg);
+                kkt_ref.assign(1, E0);
+            } else if (!free_mode && progress && !kkt_ref.empty() && E0 <= 0.9999 * kkt_ref.back()) {
+                free_mode = true;
+                kkt_ref.clear();
+            }
+            if (free_mode) {
+                kkt_ref.push_back(E0);
+                if (kkt_ref.size() > 4) kkt_ref.erase(kkt_ref.begin());
+                const double xi = mn / avg;
+                const double sg = 0.1 * std::pow(std::min(0.05 * (1 - xi) / xi, 2.0), 3);
+                mu = std::max(mu_min, std::min(sg * avg, 1e5));
+            } else if (Emu <= opt.kappa_eps * mu && mu > opt.tol / 10) {
                 mu = std::max(opt.tol / 10, std::min(opt.kappa_mu * mu, std::pow(mu, opt.theta_mu)));
+            }
+            if (mu != mu_old) {
                 filt_theta.clear();
                 filt_phi.clear();
             }
+        } else if (Emu <= opt.kappa_eps * mu && mu > opt.tol / 10) {
+            // monotone: at most one decrease per iteration
+            mu = std::max(opt.tol / 10, std::min(opt.kappa_mu * mu, std::pow(mu, opt.theta_mu)));
+            filt_theta.clear();
+            filt_phi.clear();
         }
         // 3. reduced Newton system
         double M[NMAX * NMAX], rhs[NMAX];

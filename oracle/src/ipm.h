@@ -8,7 +8,11 @@
 //   rows r = 0..m-1 (constraints, bounds [L_r, U_r], |bound| >= 1e19 means infinite) plus the
 //   n box bounds; each finite side k has slack s_k > 0 and multiplier z_k > 0;
 //   1. residuals r_d = grad f - sum_k z_k a_k, r_p = c_k(x) - s_k, errors E_0 / E_mu (Ipopt-scaled)
-//   2. monotone barrier update mu <- max(tol/10, min(kappa_mu*mu, mu^theta)) while E_mu <= kappa_eps*mu
+//   2. barrier update: monotone (default, mu_strategy 0):
+//      mu <- max(tol/10, min(kappa_mu*mu, mu^theta)) while E_mu <= kappa_eps*mu; or adaptive
+//      (option 1; Ipopt's mu_strategy "adaptive", KPR/Parameters.h:57): LOQO oracle
+//      mu = 0.1 min(0.05 (1 - xi) / xi, 2)^3 avg(s z) in free mode, with the kkt-error
+//      globalisation falling back to the monotone rule
 //   3. Newton step on the reduced 7x7 system (H + sum_k sigma_k a_k a_k^T) dx = -grad f + sum_k a_k (mu/s_k - sigma_k r_p,k)
 //   4. ds, dz, fraction-to-boundary step sizes
 //   5. Ipopt's filter line search (no restoration phase) on theta = ||c(x) - s||_1 and the
@@ -32,6 +36,10 @@ struct IpmOptions {
     double kappa_sigma = 1e10;
     double s_max = 100.0;
     double inf_bound = 1e19;
+    // barrier strategy: 0 monotone (the build's solver, GPU and CPU); 1 adaptive (Ipopt's
+    // mu_strategy "adaptive", KPR/Parameters.h:57, with the LOQO mu oracle and the kkt-error
+    // globalisation, restated in ipm.cpp; an option, see DESIGN.md §5 for why it is not the default)
+    int mu_strategy = 0;
 };
 
 struct IpmResult {

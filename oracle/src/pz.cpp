@@ -155,10 +155,12 @@ PZ PZ::rot(double cos_c, const double* cos_coeff, const uint64_t (*cos_deg)[NF *
     return r;
 }
 
-// PZsparse.cu:284-350
+// PZsparse.cu:284-350. The reference's std::sort leaves the order of equal hashes unspecified,
+// and with it the summation order of a merged group (rounding only). Here equal hashes keep their
+// generation order (stable sort), the order the HIP engines sum in (term index).
 void PZ::simplify(double thr) {
     const int n = R * C;
-    std::sort(poly.begin(), poly.end(), [](const Mono& l, const Mono& r) { return l.h < r.h; });
+    std::stable_sort(poly.begin(), poly.end(), [](const Mono& l, const Mono& r) { return l.h < r.h; });
     double red[9] = {0};
     std::vector<Mono> out;
     out.reserve(poly.size());

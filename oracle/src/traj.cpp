@@ -6,8 +6,9 @@
 // codegen) are restated through the envelope theorem: at an interior root t* of dq/dt,
 // d/dk q(t*(k), k) = dq/dk(t*) = t*^3 (6 t*^2 - 15 t* + 10); at a root of d2q/dt2,
 // d/dk qd(t*(k), k) = 30 t*^2 (t* - 1)^2. tests/test_oracle_properties.py checks both against
-// finite differences (test_jacobian_matches_finite_differences, the 28 extremum rows, and
-// test_extremum_rows_finite_differences at points with interior extrema).
+// finite differences (test_jacobian_matches_finite_differences, whose rows include the 28 extremum
+// rows), and tests/test_oracle_containment.py checks the extremum values against a dense sampling
+// of an independent Bezier point model (test_oracle_extremum_rows_bracket_the_trajectory).
 #include "traj.h"
 #include <algorithm>
 #include <cmath>

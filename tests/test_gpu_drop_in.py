@@ -81,3 +81,58 @@ def test_too_many_obstacles_fails_like_reference(tmp_path):
     r = run(str(tmp_path), 10)
     assert r.returncode != 0
     assert open(tmp_path / "armour.out").read().split() == ["-1"]
+
+
+def _outputs(path):
+    names = ["armour.out", "armour_joint_position_center.out", "armour_joint_position_radius.out",
+             "armour_control_input_radius.out", "armour_constraints.out"]
+    return {n: open(os.path.join(path, n)).read() for n in names}
+
+
+def test_served_mode_matches_in_process(tmp_path):
+    """`armour_main --serve` keeps one planner warm; a plain armour_main run then forwards its
+    buffer directory over <buffer>/armour.sock and exits with the server's status. The five output
+    files must be byte-identical to an in-process run, failures included, and a served replan
+    skips process-wide HIP initialisation."""
+    import time
+
+    T = 20
+    srv, loc = tmp_path / "srv", tmp_path / "loc"
+    srv.mkdir()
+    loc.mkdir()
+    env = dict(os.environ, ARMOUR_NUM_TIME_STEPS=str(T))
+    server = subprocess.Popen([EXE, "--serve", str(srv)], env=env, stdout=subprocess.DEVNULL,
+                              stderr=subprocess.PIPE, text=True)
+    try:
+        for _ in range(600):
+            if (srv / "armour.sock").exists() or server.poll() is not None:
+                break
+            time.sleep(0.1)
+        assert server.poll() is None and (srv / "armour.sock").exists(), "server did not start"
+        worlds = [A.example_world(), A.make_world(3, 10, profile="survey"), A.make_world(4, 10, profile="survey")]
+        walls = []
+        for world in worlds:
+            write_input(str(srv), world)
+            write_input(str(loc), world)
+            t0 = time.perf_counter()
+            rs = run(str(srv), T)
+            walls.append((time.perf_counter() - t0) * 1e3)
+            rl = subprocess.run([EXE, str(loc)], env=dict(env, ARMOUR_NO_SERVE="1"), capture_output=True, text=True,
+                                timeout=300)
+            assert rs.returncode == 0 and rl.returncode == 0, (rs.stderr, rl.stderr)
+            os_, ol = _outputs(str(srv)), _outputs(str(loc))
+            # the reported planning time (last line of armour.out) differs run to run
+            assert os_["armour.out"].split()[:-1] == ol["armour.out"].split()[:-1]
+            for n in list(os_)[1:]:
+                assert os_[n] == ol[n], n
+        # an error is served like the in-process run: -1 and a non-zero status
+        q0, qd0, qdd0, qdes, obs = A.make_world(0, 3)
+        write_input(str(srv), (q0, qd0, qdd0, qdes, np.tile(obs, (14, 1))))
+        r = run(str(srv), T)
+        assert r.returncode != 0 and open(srv / "armour.out").read().split() == ["-1"]
+        print(f"served armour_main wall time: {[round(w, 1) for w in walls]} ms")
+        assert min(walls) < 100
+    finally:
+        server.terminate()
+        server.wait(timeout=30)
+    assert not (srv / "armour.sock").exists()

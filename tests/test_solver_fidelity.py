@@ -88,3 +88,16 @@ def test_infeasible_verdict_has_no_feasible_point(i):
         best = min(best, max(0.0, -cons(r.x[:7]).min()))
     print(f"world {i}: least largest violation found {best:.3e}")
     assert best > 1e-2  # above both thresholds (torque 1e-2, collision 1e-4)
+
+
+def test_adaptive_barrier_option():
+    """IPOPT_MU_STRATEGY is "adaptive" (KPR/Parameters.h:57); the build's default barrier is monotone
+    and the adaptive one (LOQO oracle) is an option. On bench world 235 the monotone
+    solve ends in line-search failure (infeasible) while the adaptive one converges to a feasible
+    plan: the one decision of the 400 compared worlds that differs (profiles/r03_mu_study.json)"""
+    fx = load()
+    R = OraclePlanner(*bench_world(fx, 235), T=int(fx["T"]), threads=8)
+    R.reach()
+    mono, adap = R.plan(), R.plan(mu_strategy=1)
+    assert not mono["feasible"] and mono["status"] == 2 and not bool(fx["feasible"][235])
+    assert adap["feasible"] and adap["status"] == 0
