@@ -37,6 +37,9 @@ constexpr int LT = LW * LG;               // threads per workgroup
 constexpr int LKEYS = LANE_CFG_KEYS;      // LDS key capacity (global fallback beyond)
 constexpr int LSTAGE = LANE_CFG_STAGE;    // LDS staged operand hashes
 constexpr int RCH = 6;                    // reduction slots combined per round across waves
+#ifndef LANE_U99
+#define LANE_U99 1                        // groups per wave round of a 3x3 x 3x3 product
+#endif
 
 #define DI __device__ inline __attribute__((always_inline))
 
@@ -180,17 +183,18 @@ struct LSrc {
     int cnt, n, stride, comp, scaled;
     double scale;
     DI uint64_t hash(int k) const { return h[k]; }
+    // branch-free: nine loads from rows inside monomial k's block (clamped), then the selects
     DI void read(int k, bool neg, double* out, int lane) const {
         const double* base = c + (long)k * stride * LG + lane;
+        double xs[9];
+#pragma unroll
+        for (int e = 0; e < 9; e++) xs[e] = base[(long)(comp >= 0 ? comp : (e < n ? e : 0)) * LG];
 #pragma unroll
         for (int e = 0; e < 9; e++) {
-            double v = 0.0;
-            if (e < n) {
-                v = base[(long)(comp >= 0 ? comp : e) * LG];
-                if (scaled) v = scale * v;
-                if (neg) v = -v;
-            }
-            out[e] = v;
+            double v = xs[e];
+            if (scaled) v = scale * v;
+            if (neg) v = -v;
+            out[e] = e < n ? v : 0.0;
         }
     }
 };
@@ -590,7 +594,7 @@ template <int NA, int NB>
 struct GMul {
     static constexpr int NO = NA == 1 ? NB : (NB == 1 ? NA : 3 * (NB / 3));
     static constexpr int NV = NO;
-    static constexpr int U = (NA == 9 && NB == 9) ? 1 : (NA == 9 ? 3 : 4);  // groups per wave round
+    static constexpr int U = (NA == 9 && NB == 9) ? LANE_U99 : (NA == 9 ? 3 : 4);  // groups per wave round
     const double* ca;
     const double* cb;
     int na, nb;
@@ -958,19 +962,30 @@ DI void cross_const(LCtx& x, int o, int a, const CrossC& C) {
         return;
     }
     unsigned long long b = 0;
-    for (int k = x.wave; k < N; k += LW) {
+    // two monomials per trip (k, k + LW: the wave's own order, so the pruned sums accumulate as
+    // before), both monomials' rows loaded before either is used
+    for (int k = x.wave; k < N; k += 2 * LW) {
+        const int k2 = k + LW;
+        const bool has2 = k2 < N;
+        double m2[9];
         S.read(k, false, m, x.lane);
+        S.read(has2 ? k2 : k, false, m2, x.lane);
 #pragma unroll
-        for (int e = 0; e < 3; e++) out[e] = 0.0;
-        const bool keep = cross_const_mono(C, m, x.thr, out, red);
-        double* go = x.gout + (long)k * 3 * LG + x.lane;
+        for (int q = 0; q < 2; q++) {
+            if (q == 1 && !has2) break;
+            const int kk = q == 0 ? k : k2;
 #pragma unroll
-        for (int e = 0; e < 3; e++) go[(long)e * LG] = keep ? out[e] : 0.0;
-        const unsigned long long mk = ballot(keep);
-        if (x.lane == 0) {
-            x.gm[k] = mk;
-            kp[k] = mk != 0 ? 1 : 0;
-            b += (unsigned long long)__popcll(S.m[k]) * 32ull + (unsigned long long)__popcll(mk) * 32ull;
+            for (int e = 0; e < 3; e++) out[e] = 0.0;
+            const bool keep = cross_const_mono(C, q == 0 ? m : m2, x.thr, out, red);
+            double* go = x.gout + (long)kk * 3 * LG + x.lane;
+#pragma unroll
+            for (int e = 0; e < 3; e++) go[(long)e * LG] = keep ? out[e] : 0.0;
+            const unsigned long long mk = ballot(keep);
+            if (x.lane == 0) {
+                x.gm[kk] = mk;
+                kp[kk] = mk != 0 ? 1 : 0;
+                b += (unsigned long long)__popcll(S.m[kk]) * 32ull + (unsigned long long)__popcll(mk) * 32ull;
+            }
         }
     }
     if (b) atomicAdd(&x.A->bytes, b);
@@ -981,16 +996,32 @@ DI void cross_const(LCtx& x, int o, int a, const CrossC& C) {
     const LH& ho = x.H[o];
     if (ho.cnt == K) {
         double* dst = x.A->c + ho.coff * LG + x.lane;
-        for (int k = x.wave; k < N; k += LW) {
-            const bool kept = (k + 1 < N) ? kp[k + 1] != kp[k] : kp[k] != K;
-            if (!kept) continue;
-            const long pos = kp[k];
-            const double* go = x.gout + (long)k * 3 * LG + x.lane;
+        // two monomials per trip, loads first (clamped), stores of the kept ones after
+        for (int k = x.wave; k < N; k += 2 * LW) {
+            int kk[2];
+            kk[0] = k;
+            kk[1] = k + LW < N ? k + LW : k;
+            bool kept[2];
+            long pos[2];
+            double v[2][3];
 #pragma unroll
-            for (int e = 0; e < 3; e++) dst[(pos * 3 + e) * LG] = go[(long)e * LG];
-            if (x.lane == 0) {
-                x.A->h[ho.hoff + pos] = S.h[k];
-                x.A->m[ho.hoff + pos] = x.gm[k];
+            for (int q = 0; q < 2; q++) {
+                const int j = kk[q];
+                kept[q] = (q == 0 || k + LW < N) && ((j + 1 < N) ? kp[j + 1] != kp[j] : kp[j] != K);
+                pos[q] = kp[j];
+                const double* go = x.gout + (long)j * 3 * LG + x.lane;
+#pragma unroll
+                for (int e = 0; e < 3; e++) v[q][e] = go[(long)e * LG];
+            }
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                if (!kept[q]) continue;
+#pragma unroll
+                for (int e = 0; e < 3; e++) dst[(pos[q] * 3 + e) * LG] = v[q][e];
+                if (x.lane == 0) {
+                    x.A->h[ho.hoff + pos[q]] = S.h[kk[q]];
+                    x.A->m[ho.hoff + pos[q]] = x.gm[kk[q]];
+                }
             }
         }
     }
