@@ -821,6 +821,8 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
     const bool ok = ui(ho.cnt) == NG;
     double* dst = up(x.A->c) + bcast0(ho.coff) * LG + x.lane;
     const long hoff = bcast0(ho.hoff);
+    uint64_t* const Ah = up(x.A->h);
+    uint64_t* const Am = up(x.A->m);
     int base = 0;
     unsigned long long b = 0;
     unsigned long long sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -857,10 +859,14 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
         sub[5] += 1;
         sub[6] += maxsz;
         double acc[U][NV];
+        uint64_t hk[U];  // the groups' hashes, loaded with the first members (stored after the barrier)
         {
             int p0[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) p0[u] = (int)ki[lo[u]];
+            for (int u = 0; u < U; u++) {
+                p0[u] = (int)ki[lo[u]];
+                hk[u] = kh[lo[u]];
+            }
 #pragma unroll
             for (int u = 0; u < U; u++) G.term(ui(p0[u]), acc[u], x.lane);
         }
@@ -900,8 +906,8 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
 #pragma unroll
             for (int e = 0; e < n; e++) dst[(pos * n + e) * LG] = out[u][e];
             if (x.lane == 0) {
-                x.A->h[hoff + pos] = kh[lo[u]];
-                x.A->m[hoff + pos] = mk[u];
+                Ah[hoff + pos] = hk[u];
+                Am[hoff + pos] = mk[u];
                 b += (unsigned long long)__popcll(mk[u]) * (8ull + 8ull * n);
             }
         }
