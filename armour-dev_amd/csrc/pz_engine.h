@@ -280,6 +280,28 @@ AI int lower_bound_off(const uint64_t* h, int cnt, uint64_t off, uint64_t key) {
 }
 // T3 column j of a product: keys ha[i] + hb_j over i
 AI int lower_bound_col(const uint64_t* ha, int cnt, uint64_t hbj, uint64_t key) { return lower_bound_off(ha, cnt, hbj, key); }
+// RK searches over one run at once: out[u] = first k in [0, cnt) with off[u] + h[k] >= key[u].
+// Branch-free, with a halving sequence that depends on cnt only, so the RK searches' loads are in
+// flight together (one search is a chain of dependent loads; a term's rank sums many of them).
+constexpr int RK = 4;
+AI void lower_bounds(const uint64_t* h, int cnt, const uint64_t* off, const uint64_t* key, int* out) {
+    int base[RK];
+    UNR for (int u = 0; u < RK; u++) base[u] = 0;
+    if (cnt <= 0) {
+        UNR for (int u = 0; u < RK; u++) out[u] = 0;
+        return;
+    }
+    for (int n = cnt; n > 1;) {
+        const int half = n >> 1;
+        uint64_t v[RK];
+        UNR for (int u = 0; u < RK; u++) v[u] = h[base[u] + half];
+        UNR for (int u = 0; u < RK; u++) base[u] = off[u] + v[u] < key[u] ? base[u] + half : base[u];
+        n -= half;
+    }
+    uint64_t v[RK];
+    UNR for (int u = 0; u < RK; u++) v[u] = h[base[u]];
+    UNR for (int u = 0; u < RK; u++) out[u] = base[u] + (off[u] + v[u] < key[u] ? 1 : 0);
+}
 
 // term lists of an operator: kind 0 = product (PZsparse.cu:864-994: T1 a_i x B.c, T2 A.c x b_j,
 // T3 a_i x b_j with hash a_i + b_j), kind 1 = concatenation of up to 3 sources, each a full block
@@ -394,17 +416,38 @@ struct Terms {
         const int seg = p < na ? 0 : (p < base ? 1 : 2);
         int r = seg == 0 ? p : lower_bound(S[0].h, na, h1);             // T1
         r += seg == 1 ? p - na : lower_bound(S[1].h, nb, seg == 2 ? h1 : h);  // T2
+        // the T3 runs, RK searches at a time (rows i: keys h[i] + b_j; columns j: keys a_i + h[j])
         if (na <= nb) {
             int i0 = -1, j0 = 0;
             if (seg == 2) split(p - base, i0, j0);
-            for (int i = 0; i < na; i++)
-                r += i == i0 ? j0 : lower_bound_off(S[1].h, nb, S[0].h[i], i < i0 ? h1 : h);
+            for (int i = 0; i < na; i += RK) {
+                uint64_t off[RK], key[RK];
+                int lb[RK];
+                UNR for (int u = 0; u < RK; u++) {
+                    off[u] = S[0].h[i + u < na ? i + u : 0];
+                    key[u] = i + u < i0 ? h1 : h;
+                }
+                lower_bounds(S[1].h, nb, off, key, lb);
+                UNR for (int u = 0; u < RK; u++)
+                    if (i + u < na) r += i + u == i0 ? j0 : lb[u];
+            }
         } else {
-            for (int j = 0; j < nb; j++) {
-                const uint64_t hbj = S[1].h[j];
-                int lb = lower_bound_col(S[0].h, na, hbj, h);
-                if (lb < na && S[0].h[lb] + hbj == h && base + lb * nb + j < p) lb++;
-                r += lb;
+            for (int j = 0; j < nb; j += RK) {
+                uint64_t off[RK], key[RK];
+                int lb[RK];
+                UNR for (int u = 0; u < RK; u++) {
+                    off[u] = S[1].h[j + u < nb ? j + u : 0];
+                    key[u] = h;
+                }
+                lower_bounds(S[0].h, na, off, key, lb);
+                uint64_t v[RK];
+                UNR for (int u = 0; u < RK; u++) v[u] = S[0].h[lb[u] < na ? lb[u] : 0];
+                UNR for (int u = 0; u < RK; u++) {
+                    if (j + u >= nb) continue;
+                    int l = lb[u];
+                    if (l < na && v[u] + off[u] == h && base + l * nb + j + u < p) l++;
+                    r += l;
+                }
             }
         }
         return r;

@@ -10,7 +10,8 @@
 #   bench ARGS          python bench.py ARGS (the JSON line -> gpurun_out/<n>_bench.json)
 #   py SCRIPT ARGS      python -u SCRIPT ARGS
 #   stats SCRIPT ARGS   rocprofv3 --kernel-trace --stats of python SCRIPT ARGS (csv under gpurun_out/<n>_stats/)
-#   pmc 'CTRS' SCRIPT ARGS  one rocprofv3 --pmc pass (counters within one pass's block limits)
+#   pmc 'CTRS' SCRIPT ARGS  one rocprofv3 --pmc pass (counters within one pass's block limits);
+#                       SCRIPT may also be a built executable (tools/micro/...), run directly
 #   traffic TAG BATCH   FETCH_SIZE and WRITE_SIZE passes over one bench step, then tools/pmc_traffic.py
 #                       writes gpurun_out/<TAG>_reach_traffic.json for this library build
 # Environment for a step: prefix it, e.g. 'env ARMOUR_ENGINE=job py tools/reach_time.py 32'.
@@ -52,8 +53,9 @@ for step in "$@"; do
       [ $rc -eq 0 ] && python3 tools/stats_summary.py "$OUT/$tag/run_kernel_stats.csv" "$OUT/$tag.txt" "$step" && head -14 "$OUT/$tag.txt" ;;
     pmc)
       ctrs=$1; shift
+      prog=(python3 "$R/$1"); [[ "$1" == *.py ]] || prog=("$R/$1")
       (cd /tmp && env "${envs[@]}" timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv \
-          -d "$OUT/$tag" -o run -- python3 "$R/$1" "${@:2}") > "$OUT/$tag.log" 2>&1
+          -d "$OUT/$tag" -o run -- "${prog[@]}" "${@:2}") > "$OUT/$tag.log" 2>&1
       rc=$? ;;
     traffic)
       ttag=$1; batch=$2
