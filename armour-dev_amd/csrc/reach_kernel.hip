@@ -11,7 +11,7 @@ namespace armour {
 #ifndef REACH_CFG_THREADS
 #define REACH_CFG_THREADS 128
 #define REACH_CFG_KEYS 1024
-#define REACH_CFG_STAGE 1280
+#define REACH_CFG_STAGE 1184
 #define REACH_CFG_WG_PER_CU 4
 #endif
 #ifndef REACH_CFG_WAVES_PER_SIMD
