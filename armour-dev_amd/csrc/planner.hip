@@ -82,6 +82,7 @@ struct armour_planner {
     double* d_tables = nullptr;  // ARMTD: offline JRS tables [W][NF][6][T]
     long job_max = 0;         // batches of at most this many jobs (W x T) run on the per-job engine
     bool job_fits = true;     // the reach program's payload pool fits the per-job engine's LDS
+    bool job_narrow = false;  // ARMOUR_REACH_WIDE=0 (diagnostics): small batches on the 128-thread kernel too
     bool eval_f32 = false;    // ARMOUR_EVAL_F32: fp32 constraint evaluation (tolerance study only)
     bool eval_full = false;   // ARMOUR_EVAL_FULL: always the full-capacity evaluation kernels
     // largest link / torque k-monomial counts of the last reach (both engines record them in
@@ -128,7 +129,7 @@ static int row_chunk() {
 constexpr int RETRY_SCALE = 4;
 
 // largest batch (jobs = worlds x T) that runs on the per-job engine; measured crossover, DESIGN.md §4
-constexpr long JOB_ENGINE_JOBS = 3072;
+constexpr long JOB_ENGINE_JOBS = 5120;
 
 static int planner_init(armour_planner* p, const armour_config* cfg, const armour_robot* robot, bool armtd = false) {
     p->cfg = *cfg;
@@ -242,8 +243,16 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     {
         // ARMOUR_REACH_WG_PER_CU (diagnostics): fewer resident workgroups per CU than the 4 that fit
         const char* wg = std::getenv("ARMOUR_REACH_WG_PER_CU");
-        const int per = wg ? std::atoi(wg) : REACH_WG_PER_CU;
-        p->reach_grid = (per >= 1 && per <= REACH_WG_PER_CU ? per : REACH_WG_PER_CU) * p->ncu;
+        int fit = REACH_WG_PER_CU;  // as many as the CU's LDS holds (a persistent grid larger than
+        {                           // the resident set would run its last workgroups one job late)
+            hipFuncAttributes fa{};
+            int lds_cu = 0;
+            HIPCK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&reach_kernel<REACH_THREADS>)));
+            HIPCK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+            if (fa.sharedSizeBytes > 0) fit = std::max(1, std::min<int>(fit, (int)(lds_cu / fa.sharedSizeBytes)));
+        }
+        const int per = wg ? std::atoi(wg) : fit;
+        p->reach_grid = (per >= 1 && per <= fit ? per : fit) * p->ncu;
     }
     // Engine choice per batch. The bundle engine (lane_kernel.hip) runs 64 jobs per workgroup and
     // fills the chip from ~2 x CUs x 64 jobs on, but one bundle takes ~18 ms whatever its size. The
@@ -254,6 +263,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         const char* eng = std::getenv("ARMOUR_ENGINE");
         const char* jm = std::getenv("ARMOUR_JOB_ENGINE_JOBS");
         p->job_max = jm ? std::atol(jm) : JOB_ENGINE_JOBS;
+        const char* wide = std::getenv("ARMOUR_REACH_WIDE");
+        p->job_narrow = wide && std::atoi(wide) == 0;
         if (eng && std::strcmp(eng, "job") == 0) p->job_max = (long)Wm * T;
         if ((eng && std::strcmp(eng, "lane") == 0) || !p->job_fits) p->job_max = 0;
         p->has_job = p->job_max > 0;
@@ -531,7 +542,11 @@ static int run_reach(armour_planner* p) {
         const int lg = (int)(bundles < p->lane_grid ? bundles : p->lane_grid);
         hipLaunchKernelGGL(lane::lane_reach_kernel, dim3(lg), dim3(lane::LT), 0, rs, p->d_rp, la, p->ro);
     } else {
-        hipLaunchKernelGGL(reach_kernel, dim3(grid), dim3(REACH_THREADS), 0, rs, p->d_rp, ra, p->ro);
+        // a batch that fits the chip in one round at two jobs per CU takes the wide kernel
+        if (jobs <= (long)REACH_WIDE_PER_CU * p->ncu && !p->job_narrow)
+            hipLaunchKernelGGL(reach_kernel<REACH_WIDE_THREADS>, dim3(grid), dim3(REACH_WIDE_THREADS), 0, rs, p->d_rp, ra, p->ro);
+        else
+            hipLaunchKernelGGL(reach_kernel<REACH_THREADS>, dim3(grid), dim3(REACH_THREADS), 0, rs, p->d_rp, ra, p->ro);
     }
     HIPCK(hipGetLastError());
     HIPCK(hipEventRecord(p->ev[4], rs));

@@ -1,9 +1,12 @@
-// armour-mi355x — reach-set kernel: one 128-thread workgroup per (world, time interval) job.
+// armour-mi355x — reach-set kernel: one workgroup per (world, time interval) job.
 // Persistent grid: each workgroup walks jobs job = blockIdx.x + k * gridDim.x, interprets the
 // reach program (reach.h) for each, and owns a private HBM arena (monomial storage) plus a global
-// fallback sort buffer for products larger than the LDS key buffer. LDS (< 40 KB) holds the PZ
-// handle table and payload pool, the (hash, index) keys and the operand staging buffer, so four
-// workgroups (eight waves) fit per CU — the VGPR budget of two waves per SIMD.
+// fallback sort buffer for products larger than the LDS key buffer. LDS (<= 40 KB) holds the PZ
+// handle table and payload pool, the (hash, index) keys and the operand staging buffer.
+// Two widths of the same kernel: 128 threads, four workgroups (eight waves) per CU, for batches
+// up to JOB_ENGINE_JOBS; 256 threads, two per CU, for batches that fit the chip in one round
+// (<= 2 x CUs jobs: the drop-in's single plan), where a job's latency is the reach time and the
+// extra waves shorten the large operators' passes. Both at the VGPR budget of two waves per SIMD.
 #include "reach.h"
 
 namespace armour {
@@ -11,13 +14,15 @@ namespace armour {
 #ifndef REACH_CFG_THREADS
 #define REACH_CFG_THREADS 128
 #define REACH_CFG_KEYS 1024
-#define REACH_CFG_STAGE 1184
+#define REACH_CFG_STAGE 1152
 #define REACH_CFG_WG_PER_CU 4
 #endif
 #ifndef REACH_CFG_WAVES_PER_SIMD
 #define REACH_CFG_WAVES_PER_SIMD 2
 #endif
 constexpr int REACH_THREADS = REACH_CFG_THREADS;   // two waves per job, four jobs resident per CU
+constexpr int REACH_WIDE_THREADS = 256;            // four waves per job, two jobs resident per CU
+constexpr int REACH_WIDE_PER_CU = 2;
 constexpr int KEY_CAP_LDS = REACH_CFG_KEYS;
 constexpr int STAGE_DOUBLES = REACH_CFG_STAGE;
 constexpr int REACH_WG_PER_CU = REACH_CFG_WG_PER_CU;
@@ -131,16 +136,17 @@ struct ReachArgs {
     double* dump;               // optional op-by-op state of job 0 (null: off)
 };
 
-// 2 waves per SIMD: 256 registers per lane (VGPR + AGPR), four 2-wave workgroups per CU
-__global__ __attribute__((amdgpu_flat_work_group_size(REACH_THREADS, REACH_THREADS), amdgpu_waves_per_eu(REACH_CFG_WAVES_PER_SIMD, REACH_CFG_WAVES_PER_SIMD))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
+// 2 waves per SIMD: 256 registers per lane (VGPR + AGPR); NT threads per job
+template <int NT>
+__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(REACH_CFG_WAVES_PER_SIMD, REACH_CFG_WAVES_PER_SIMD))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
     __shared__ PZH H[MAX_SLOTS];
     __shared__ double pool[POOL_DOUBLES + 9];  // + 9: header reads of a full 3x3 past a small slot
     __shared__ uint64_t kh[KEY_CAP_LDS];
     __shared__ uint32_t ki[KEY_CAP_LDS];
     __shared__ int kp[KEY_CAP_LDS];
     __shared__ double stage[STAGE_DOUBLES];
-    __shared__ double red[(REACH_THREADS / 64) * 18];
-    __shared__ int iscan[REACH_THREADS / 64];
+    __shared__ double red[(NT / 64) * 18];
+    __shared__ int iscan[NT / 64];
     __shared__ Arena arena;
     __shared__ int err;
     __shared__ JrsJoint jrs[NF];

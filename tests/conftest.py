@@ -51,19 +51,27 @@ def world_of(fx):
 
 class engine:
     """context manager: planners created inside use reach engine `name` ("lane": the bundle
-    engine, "job": the per-job engine; planner.hip picks by batch size otherwise)"""
+    engine; "job": the per-job engine, whose batches of at most 2 x CUs jobs take its 256-thread
+    kernel; "narrow": the per-job engine's 128-thread kernel at every batch size; None: planner.hip
+    picks by batch size)"""
+
+    VARS = ("ARMOUR_ENGINE", "ARMOUR_REACH_WIDE")
 
     def __init__(self, name):
         self.name = name
 
     def __enter__(self):
-        self.prev = os.environ.get("ARMOUR_ENGINE")
-        if self.name:
+        self.prev = {k: os.environ.get(k) for k in self.VARS}
+        if self.name == "narrow":
+            os.environ["ARMOUR_ENGINE"] = "job"
+            os.environ["ARMOUR_REACH_WIDE"] = "0"
+        elif self.name:
             os.environ["ARMOUR_ENGINE"] = self.name
         return self
 
     def __exit__(self, *exc):
-        if self.prev is None:
-            os.environ.pop("ARMOUR_ENGINE", None)
-        else:
-            os.environ["ARMOUR_ENGINE"] = self.prev
+        for k, v in self.prev.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v

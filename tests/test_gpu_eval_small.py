@@ -6,23 +6,25 @@ import numpy as np
 import pytest
 
 import armour_amd as A
+from conftest import engine
 from test_boundary import load, world
 from test_gpu_plane_cache import check_eval, check_plan, env
 
 pytestmark = pytest.mark.gpu
 
 
-def planners(T, O, W):
-    P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
-    with env("ARMOUR_EVAL_FULL", "1"):
-        Q = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+def planners(T, O, W, eng=None):
+    with engine(eng):
+        P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+        with env("ARMOUR_EVAL_FULL", "1"):
+            Q = A.Planner(T=T, max_obstacles=O, max_worlds=W)
     return P, Q
 
 
 def test_eval_small_survey_worlds():
-    T, O, W = 100, 20, 40  # 4000 jobs: the bundle engine, which records the PZ sizes
+    T, O, W = 100, 20, 40
     worlds = [A.make_world(3000 + s, O, profile="survey") for s in range(W)]
-    P, Q = planners(T, O, W)
+    P, Q = planners(T, O, W, "lane")  # the bundle engine records the PZ sizes
     check_eval(P, Q, worlds, np.random.default_rng(5), n=2)
     check_plan(P, Q, worlds)
     occ = P.occupancy()

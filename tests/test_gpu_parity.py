@@ -26,7 +26,7 @@ def collision_rows(T, O, NJ):
     return slice(7 * T, 7 * T + NJ * T * O)
 
 
-ENGINES = ["lane", "job"]  # both reach engines (planner.hip picks by batch size)
+ENGINES = ["lane", "job", "narrow"]  # both reach engines, the per-job one at both widths (conftest.engine)
 
 
 @pytest.mark.parametrize("eng", ENGINES)
