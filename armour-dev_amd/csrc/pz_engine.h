@@ -454,17 +454,26 @@ struct Terms {
     }
 };
 
-// copy the sources into LDS (hashes, then effective coefficient rows), if they fit; uniform
-// decision. The caller's barrier publishes the staged copy.
+// copy the sources into LDS (hashes, then effective coefficient rows), if they fit; else the
+// hashes alone, if they fit (the key order's searches are chains of dependent hash loads, the
+// group passes' coefficient loads are independent). Uniform decision; the caller's barrier
+// publishes the staged copy.
 AI void stage_sources(Ctx& x, Terms& T) {
-    int need = 0;
-    UNR for (int s = 0; s < 3; s++) if (s < T.ns) need += T.S[s].cnt * (1 + T.S[s].n);
-    if (need > x.stage_cap) return;
+    int need = 0, need_h = 0;
+    UNR for (int s = 0; s < 3; s++) if (s < T.ns) { need += T.S[s].cnt * (1 + T.S[s].n); need_h += T.S[s].cnt; }
+    if (need_h > x.stage_cap) return;
+    const bool full = need <= x.stage_cap;
     double* base = x.stage;
     UNR for (int s = 0; s < 3; s++) {
         if (s >= T.ns) continue;
         Src& S = T.S[s];
         uint64_t* hs = (uint64_t*)base;
+        if (!full) {
+            for (int k = x.g.tid; k < S.cnt; k += x.g.n) hs[k] = S.h[k];
+            S.h = hs;
+            base += S.cnt;
+            continue;
+        }
         double* cs = base + S.cnt;
         // two monomials per thread per round, every load of a round issued before its stores
         for (int k = x.g.tid; k < S.cnt; k += 2 * x.g.n) {
