@@ -43,9 +43,9 @@ struct LaneArgs {
 };
 
 #ifndef LANE_CFG_WPE
-#define LANE_CFG_WPE 2
+#define LANE_CFG_WPE 3
 #endif
-// LANE_CFG_WPE waves per SIMD (2: 256 VGPRs): e.g. one 8-wave or two 4-wave bundles per CU
+// LANE_CFG_WPE waves per SIMD (3: 168 VGPRs, three 4-wave bundles per CU; 2: 256 VGPRs)
 __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_eu(LANE_CFG_WPE, LANE_CFG_WPE))) void lane_reach_kernel(const RobotParams* __restrict__ rpp, LaneArgs a, ReachOut out) {
     __shared__ LH H[MAX_SLOTS];
     __shared__ uint64_t kh[LKEYS];

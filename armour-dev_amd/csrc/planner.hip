@@ -315,11 +315,20 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             return rc;
     }
     if (p->has_lane) {
-        // one resident bundle workgroup per CU, each with its own arena; sizes from the measured
-        // per-job use (~16.5k monomials) times the union inflation, with margin
+        // LANE_WG_PER_CU resident bundle workgroups per CU (as many as the CU's LDS holds), each
+        // with its own arena; sizes from the measured per-job use (~16.5k monomials) times the union
+        // inflation, with margin
         lane::LaneArgs& la = p->la;
         const long bundles = ((long)Wm * T + lane::LG - 1) / lane::LG;
-        const long slots = (long)p->reach_cus * lane::LANE_WG_PER_CU;
+        int per_cu = lane::LANE_WG_PER_CU;
+        {
+            hipFuncAttributes fa{};
+            int lds_cu = 0;
+            HIPCK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&lane::lane_reach_kernel)));
+            HIPCK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+            if (fa.sharedSizeBytes > 0) per_cu = std::max(1, std::min<int>(per_cu, (int)(lds_cu / fa.sharedSizeBytes)));
+        }
+        const long slots = (long)p->reach_cus * per_cu;
         p->lane_grid = (int)(bundles < slots ? bundles : slots);
         const char* hc = std::getenv("ARMOUR_LANE_HCAP");
         const char* cc = std::getenv("ARMOUR_LANE_CCAP");
