@@ -23,23 +23,11 @@ namespace lane {
 
 constexpr int LG = 64;  // jobs per bundle = lanes per wave
 
-// Three resident 4-wave bundles per CU (LDS 51.6 KB each, 168 VGPRs at three waves per SIMD). Alone
-// on the GPU two bundles per CU at 256 VGPRs and 2048 LDS keys run a 327-world launch faster (33.4
-// against 38.9 ms), but under concurrent planners, whose kernels need room on the CUs a reach launch
-// holds, this shape gives the higher throughput (bench 5187 -> 5347 plans/s).
 #ifndef LANE_CFG_WAVES
 #define LANE_CFG_WAVES 4
-#define LANE_CFG_KEYS 1024
-#define LANE_CFG_STAGE 1024
 #endif
-#ifndef LANE_CFG_WG_PER_CU
-#define LANE_CFG_WG_PER_CU 3  // resident bundles per CU
-#endif
-constexpr int LANE_WG_PER_CU = LANE_CFG_WG_PER_CU;
 constexpr int LW = LANE_CFG_WAVES;        // waves per workgroup
 constexpr int LT = LW * LG;               // threads per workgroup
-constexpr int LKEYS = LANE_CFG_KEYS;      // LDS key capacity (global fallback beyond)
-constexpr int LSTAGE = LANE_CFG_STAGE;    // LDS staged operand hashes
 constexpr int RCH = 6;                    // reduction slots combined per round across waves
 #ifndef LANE_U99
 #define LANE_U99 1                        // groups per wave round of a 3x3 x 3x3 product

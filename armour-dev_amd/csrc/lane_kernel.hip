@@ -2,9 +2,15 @@
 // per bundle of 64 consecutive (world, interval) jobs, lane = job. Persistent grid over bundles;
 // each resident workgroup owns an HBM arena (union hashes, presence masks, [row][64] coefficients),
 // a header pool ([row][64]) and global key buffers for operators beyond the LDS key capacity. LDS
-// (~78 KB) holds the handle table, keys, group heads, staged operand hashes and the cross-wave
-// reduction rows: two workgroups per CU (two waves per SIMD), so one bundle's barriers and serial
-// header work overlap the other's group rounds (measured: 8.5 % faster than one 8-wave bundle).
+// holds the handle table, keys, group heads, staged operand hashes and the cross-wave reduction
+// rows; several resident workgroups per CU overlap one bundle's barriers and serial header work
+// with the others' group rounds. Two shapes of the same kernel (identical arithmetic: the key and
+// stage capacities only decide what lives in LDS):
+//   LaneWide:  2048 LDS keys / staged hashes, 78 KB LDS, 256 VGPRs: two bundles per CU; the faster
+//              one for a planner alone on the GPU whose batch fits one round of two per CU;
+//   LaneDense: 1024 / 1024, 51.6 KB, 168 VGPRs (more spills): three per CU; faster per world once a
+//              batch fills three per CU, and under concurrent planners, whose kernels then find
+//              room on the CUs a reach launch holds.
 #include "lane_engine.h"
 
 namespace armour {
@@ -42,17 +48,22 @@ struct LaneArgs {
     int nlist;
 };
 
-#ifndef LANE_CFG_WPE
-#define LANE_CFG_WPE 3
-#endif
-// LANE_CFG_WPE waves per SIMD (3: 168 VGPRs, three 4-wave bundles per CU; 2: 256 VGPRs)
-__global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_eu(LANE_CFG_WPE, LANE_CFG_WPE))) void lane_reach_kernel(const RobotParams* __restrict__ rpp, LaneArgs a, ReachOut out) {
+struct LaneWide {
+    static constexpr int KEYS = 2048, STAGE = 2048, WPE = 2, PER_CU = 2;
+};
+struct LaneDense {
+    static constexpr int KEYS = 1024, STAGE = 1024, WPE = 3, PER_CU = 3;
+};
+
+// S::WPE waves per SIMD (2: 256 VGPRs, 3: 168)
+template <class S>
+__global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_eu(S::WPE, S::WPE))) void lane_reach_kernel(const RobotParams* __restrict__ rpp, LaneArgs a, ReachOut out) {
     __shared__ LH H[MAX_SLOTS];
-    __shared__ uint64_t kh[LKEYS];
-    __shared__ uint32_t ki[LKEYS];
-    __shared__ int kp[LKEYS + 1];
-    __shared__ int gp[LKEYS + 1];
-    __shared__ uint64_t stage[LSTAGE];
+    __shared__ uint64_t kh[S::KEYS];
+    __shared__ uint32_t ki[S::KEYS];
+    __shared__ int kp[S::KEYS + 1];
+    __shared__ int gp[S::KEYS + 1];
+    __shared__ uint64_t stage[S::STAGE];
     __shared__ uint64_t rmask[128];
     __shared__ double red[(LW - 1) * RCH * LG];
     __shared__ double scr[2 * NF * LG];
@@ -71,7 +82,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     x.H = H;
     x.pool = a.pool + wg * a.pool_rows * LG;
     x.A = &arena;
-    x.kh = kh; x.ki = ki; x.kp = kp; x.gp = gp; x.cap_lds = LKEYS;
+    x.kh = kh; x.ki = ki; x.kp = kp; x.gp = gp; x.cap_lds = S::KEYS;
     x.gkh = a.gkh + wg * a.gcap;
     x.gki = a.gki + wg * a.gcap;
     x.gkp = a.gkp + wg * (a.gcap + 1);
@@ -82,7 +93,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     x.cap_out = a.ocap;
     x.rmask = rmask;
     x.stage = stage;
-    x.stage_cap = LSTAGE;
+    x.stage_cap = S::STAGE;
     x.red = red;
     x.scr = scr;
     x.iscan = iscan;

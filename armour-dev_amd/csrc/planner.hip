@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -42,6 +43,10 @@ hipError_t dalloc(T** p, size_t n) {
     return hipMalloc((void**)p, sizeof(T) * (n > 0 ? n : 1));
 }
 }  // namespace
+
+// planners alive per device (armour_create / armour_destroy): the bundle kernel's shape depends on
+// whether the GPU is shared (lane_shape_for)
+static std::atomic<int> g_planners[64];
 
 struct armour_planner {
     armour_config cfg;
@@ -89,7 +94,12 @@ struct armour_planner {
     // occ[3], occ[4], published with the error flags), and the first launch's occupancy
     unsigned long long h_occ[8] = {};
     int mono_max[2] = {CAP_LM, CAP_UM};
-    int lane_grid = 0;
+    int lane_grid = 0;        // workgroups with an arena: the larger (dense) shape's resident set
+    int lane_slots[2] = {0, 0};  // resident bundle workgroups of the wide / dense kernel shape
+    int lane_shape = -1;      // ARMOUR_LANE_SHAPE: 0 wide, 1 dense, -1 chosen per launch
+    int last_shape = 0;       // shape of the last first launch (a capacity retry uses it too)
+    int dev = 0;              // the planner's device
+    bool counted = false;     // counted in g_planners[dev]
     lane::LaneArgs la;
 
     // nlp
@@ -142,6 +152,9 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     if (cfg->device >= 0) HIPCK(hipSetDevice(cfg->device));
     int dev = 0;
     HIPCK(hipGetDevice(&dev));
+    p->dev = dev;
+    g_planners[dev & 63]++;
+    p->counted = true;
     HIPCK(hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (robot) {
         if (!robot_from_tables(*robot, p->rp))
@@ -320,15 +333,24 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         // inflation, with margin
         lane::LaneArgs& la = p->la;
         const long bundles = ((long)Wm * T + lane::LG - 1) / lane::LG;
-        int per_cu = lane::LANE_WG_PER_CU;
         {
-            hipFuncAttributes fa{};
             int lds_cu = 0;
-            HIPCK(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&lane::lane_reach_kernel)));
             HIPCK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
-            if (fa.sharedSizeBytes > 0) per_cu = std::max(1, std::min<int>(per_cu, (int)(lds_cu / fa.sharedSizeBytes)));
+            const void* fn[2] = {reinterpret_cast<const void*>(&lane::lane_reach_kernel<lane::LaneWide>),
+                                 reinterpret_cast<const void*>(&lane::lane_reach_kernel<lane::LaneDense>)};
+            const int want[2] = {lane::LaneWide::PER_CU, lane::LaneDense::PER_CU};
+            for (int k = 0; k < 2; k++) {
+                hipFuncAttributes fa{};
+                HIPCK(hipFuncGetAttributes(&fa, fn[k]));
+                int per_cu = want[k];
+                if (fa.sharedSizeBytes > 0) per_cu = std::max(1, std::min<int>(per_cu, (int)(lds_cu / fa.sharedSizeBytes)));
+                p->lane_slots[k] = p->reach_cus * per_cu;
+            }
+            const char* sh = std::getenv("ARMOUR_LANE_SHAPE");
+            if (sh && std::strcmp(sh, "wide") == 0) p->lane_shape = 0;
+            if (sh && std::strcmp(sh, "dense") == 0) p->lane_shape = 1;
         }
-        const long slots = (long)p->reach_cus * per_cu;
+        const long slots = std::max(p->lane_slots[0], p->lane_slots[1]);
         p->lane_grid = (int)(bundles < slots ? bundles : slots);
         const char* hc = std::getenv("ARMOUR_LANE_HCAP");
         const char* cc = std::getenv("ARMOUR_LANE_CCAP");
@@ -516,6 +538,26 @@ static int upload_armtd(armour_planner* p, int W, const armour_armtd_world* worl
     return upload_worlds(p, W, base.data());  // ends in a synchronisation: tab / kr outlive the copies
 }
 
+// Bundle kernel shape of a launch of `bundles` bundles (lane_kernel.hip): the dense shape (three
+// per CU) when the batch does not fit one round of the wide shape (two per CU), or when other
+// planners share the device and the batch holds more than one bundle per CU; else the wide shape.
+// Measured: three planners x 327 worlds dense 5324-5363 against 5187 plans/s;
+// three planners x 85 worlds (config 4's 256-world job) wide 63.5 against 72.1 ms.
+static int lane_shape_for(armour_planner* p, long bundles) {
+    int shape = p->lane_shape;
+    if (shape < 0)
+        shape = (bundles > p->lane_slots[0] || (g_planners[p->dev & 63].load() > 1 && bundles > p->reach_cus)) ? 1 : 0;
+    p->last_shape = shape;
+    return shape;
+}
+static void launch_lane(int shape, int grid, hipStream_t s, const RobotParams* rp, const lane::LaneArgs& la,
+                        const ReachOut& ro) {
+    if (shape == 1)
+        hipLaunchKernelGGL(lane::lane_reach_kernel<lane::LaneDense>, dim3(grid), dim3(lane::LT), 0, s, rp, la, ro);
+    else
+        hipLaunchKernelGGL(lane::lane_reach_kernel<lane::LaneWide>, dim3(grid), dim3(lane::LT), 0, s, rp, la, ro);
+}
+
 // reach set for the uploaded batch. The whole phase is three kernel launches on the reach stream
 // (JRS, reach, and a capacity retry when needed) and one event wait: jrs_kernel zeroes the
 // counters, the reach kernel's last workgroup publishes them in mapped host memory
@@ -548,8 +590,10 @@ static int run_reach(armour_planner* p) {
         la.T = p->T;
         la.jrs = p->d_jrs;
         const long bundles = (jobs + lane::LG - 1) / lane::LG;
-        const int lg = (int)(bundles < p->lane_grid ? bundles : p->lane_grid);
-        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3(lg), dim3(lane::LT), 0, rs, p->d_rp, la, p->ro);
+        const int shape = lane_shape_for(p, bundles);
+        const long slots = std::min<long>(p->lane_slots[shape], p->lane_grid);
+        const int lg = (int)(bundles < slots ? bundles : slots);
+        launch_lane(shape, lg, rs, p->d_rp, la, p->ro);
     } else {
         // a batch that fits the chip in one round at two jobs per CU takes the wide kernel
         if (jobs <= (long)REACH_WIDE_PER_CU * p->ncu && !p->job_narrow)
@@ -598,8 +642,7 @@ static int run_reach(armour_planner* p) {
         HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, rs));
         const long bundles = ((long)retry.size() * p->T + lane::LG - 1) / lane::LG;
         const long g = std::max(p->lane_grid, RETRY_SCALE) / RETRY_SCALE;
-        hipLaunchKernelGGL(lane::lane_reach_kernel, dim3((int)(bundles < g ? bundles : g)), dim3(lane::LT), 0, rs,
-                           p->d_rp, la, p->ro);
+        launch_lane(p->last_shape, (int)(bundles < g ? bundles : g), rs, p->d_rp, la, p->ro);
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(p->ev[5], rs));
         HIPCK(hipEventSynchronize(p->ev[5]));
@@ -931,6 +974,7 @@ void armour_destroy(armour_planner* p) {
         if (p->rstream && p->rstream != p->stream) (void)hipStreamDestroy(p->rstream);
         (void)hipStreamDestroy(p->stream);
     }
+    if (p->counted) g_planners[p->dev & 63]--;
     delete p;
 }
 

@@ -28,3 +28,19 @@ def test_cu_masked_reach_stream_plans_bitwise(eng):
         for a, b in zip(ra, rb):
             np.testing.assert_array_equal(a["k_opt"], b["k_opt"])
             assert a["iterations"] == b["iterations"]
+
+
+def test_bundle_kernel_shapes_plan_bitwise():
+    """the bundle kernel's two LDS / register shapes (lane_kernel.hip LaneWide, LaneDense; planner.hip
+    picks by device sharing and batch size) hold the same arithmetic: plans bitwise equal"""
+    T, O, W = 100, 20, 24
+    worlds = [A.make_world(4100 + s, O, profile="survey") for s in range(W)]
+    with engine("lane"):
+        with env("ARMOUR_LANE_SHAPE", "wide"):
+            P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+        with env("ARMOUR_LANE_SHAPE", "dense"):
+            Q = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    check_plan(P, Q, worlds)
+    for w in range(W):
+        np.testing.assert_array_equal(P.link_generators(w), Q.link_generators(w))
+        np.testing.assert_array_equal(P.torque_radius(w), Q.torque_radius(w))
