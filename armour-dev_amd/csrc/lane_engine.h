@@ -80,7 +80,7 @@ struct LCtx {
     uint64_t* stage;       // LDS staged operand hashes
     int stage_cap;
     double* red;           // LDS [(LW - 1) * RCH][LG]
-    double* scr;           // LDS [2 * NF][LG]: per-job disturbance / reduce radii
+    double* scr;           // [2 * NF][LG] (pool rows): per-job disturbance / reduce radii
     int* iscan;            // LDS [LW]
     int* err;              // LDS
     int* occ;              // LDS [4]: largest operator term count, link / torque k-only monomials,

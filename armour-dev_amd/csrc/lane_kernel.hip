@@ -6,9 +6,9 @@
 // rows; several resident workgroups per CU overlap one bundle's barriers and serial header work
 // with the others' group rounds. Two shapes of the same kernel (identical arithmetic: the key and
 // stage capacities only decide what lives in LDS):
-//   LaneWide:  2048 LDS keys / staged hashes, 78 KB LDS, 256 VGPRs: two bundles per CU; the faster
+//   LaneWide:  2048 LDS keys / staged hashes, 73 KB LDS, 256 VGPRs: two bundles per CU; the faster
 //              one for a planner alone on the GPU whose batch fits one round of two per CU;
-//   LaneDense: 1024 / 1024, 51.6 KB, 168 VGPRs (more spills): three per CU; faster per world once a
+//   LaneDense: 1344 / 1024, 50.8 KB, 168 VGPRs (more spills): three per CU; faster per world once a
 //              batch fills three per CU, and under concurrent planners, whose kernels then find
 //              room on the CUs a reach launch holds.
 #include "lane_engine.h"
@@ -23,7 +23,7 @@ struct LaneArgs {
     int nops;
     const int* slot_off;   // payload rows of every handle slot in the pool
     int nslots;
-    long pool_rows;        // per workgroup
+    long pool_rows;        // per workgroup (the last 2 NF rows: torque-radius scratch)
     double* pool;          // [grid][pool_rows][LG]
     uint64_t* arena_h;     // [grid][hcap]
     uint64_t* arena_m;     // [grid][hcap]
@@ -52,7 +52,7 @@ struct LaneWide {
     static constexpr int KEYS = 2048, STAGE = 2048, WPE = 2, PER_CU = 2;
 };
 struct LaneDense {
-    static constexpr int KEYS = 1024, STAGE = 1024, WPE = 3, PER_CU = 3;
+    static constexpr int KEYS = 1344, STAGE = 1024, WPE = 3, PER_CU = 3;
 };
 
 // S::WPE waves per SIMD (2: 256 VGPRs, 3: 168)
@@ -66,7 +66,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     __shared__ uint64_t stage[S::STAGE];
     __shared__ uint64_t rmask[128];
     __shared__ double red[(LW - 1) * RCH * LG];
-    __shared__ double scr[2 * NF * LG];
     __shared__ int iscan[LW];
     __shared__ LArena arena;
     __shared__ int err;
@@ -95,7 +94,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     x.stage = stage;
     x.stage_cap = S::STAGE;
     x.red = red;
-    x.scr = scr;
+    x.scr = x.pool + (a.pool_rows - 2 * NF) * LG;  // torque scratch: the pool's last 2 NF rows
     x.iscan = iscan;
     x.err = &err;
     x.occ = occ;

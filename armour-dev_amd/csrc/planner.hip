@@ -364,7 +364,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             pb.build(p->rp, p->armtd);
             (void)pb.slot_offsets(&pool);
         }
-        la.pool_rows = pool + 9;
+        la.pool_rows = pool + 9 + 2 * NF;  // + the torque-radius scratch rows (lane_kernel.hip)
         // buffers of at least RETRY_SCALE workgroups, so even a one-world batch has a capacity retry
         const size_t G = (size_t)std::max(p->lane_grid, RETRY_SCALE), LGs = lane::LG;
         if ((rc = p->alloc(&la.pool, G * la.pool_rows * LGs)) || (rc = p->alloc(&la.arena_h, G * la.hcap)) ||
