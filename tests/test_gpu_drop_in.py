@@ -62,6 +62,15 @@ def test_example_world_protocol(tmp_path):
     np.testing.assert_allclose(cons[:m], P.constraints(0), rtol=1e-5, atol=1e-5)
     b = P.joint_bounds()
     np.testing.assert_allclose(cons[m:], b, rtol=1e-5)
+    # the reference's writers are ofstreams at setprecision(10) / (6) (armour_main.cu:319-398): every
+    # number is printf's %.10g / %.6g rendering of itself, space / newline separated as there
+    for name, prec in (("armour_joint_position_center.out", 10), ("armour_joint_position_radius.out", 10),
+                       ("armour_control_input_radius.out", 10), ("armour_constraints.out", 6)):
+        text = open(tmp_path / name).read()
+        toks = text.split()
+        assert toks and all(t == "%.*g" % (prec, float(t)) for t in toks), name
+        if prec == 10:
+            assert all(line.endswith(" ") for line in text.splitlines()), name
     # per joint [lb + qe, ub - qe], then [-v + qde, v - qde] (armour_main.cu:385-396)
     assert np.all(b[0:14:2] > KINOVA.state_lb) and np.all(b[1:14:2] < KINOVA.state_ub)
     np.testing.assert_allclose(b[14::2], -b[15::2])
