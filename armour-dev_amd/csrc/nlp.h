@@ -112,12 +112,17 @@ struct NlpDev {
     // memory, read by the host one iteration later)
     unsigned* lrun_out;
     int* nrun_flag;
+    int* bt_flag;           // mapped host: worlds of this iteration that searched past round 0
     // Speculative line-search round: the values (g, f) of the remaining K = max_ls - 1 trial points
     // of every world still searching after round 0, [list entry i][trial k] (eval_trials_kernel,
     // ipm_world_Cs); the trial that ends the search is then evaluated in full into the world's trial
     // slot (eval_kernel_t mode 5).
     int K;
     double *gs, *fs, *partial_s;
+    // sync-free tail, one-round line search (planner.hip run_solver): pass B's world step runs in
+    // ipm_world_Cs_all; the trial passes before it take the first step from pass B's partials
+    // (pass_b_alpha) and every running world searches
+    int b_in_cs;
     // Certified plane cache (plane_cache_kernel). The 36 planes of a buffered
     // obstacle and their offsets d, delta do not depend on x; only A . c(x) does. For every
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in

@@ -1123,20 +1123,21 @@ template __global__ void eval_kernel_t<double, true, true>(NlpDev, int);
 // LM, UM, UB as eval_body; the staging buffer then holds the (trial, pair) keys, K * NP <= UB
 constexpr int UB_TS = EV_MAXK * 280;   // small variant: 9 trials of up to 280 pairs (7 links x 40 obstacles)
 static_assert(UB_TS >= MAX_J * LM_S * 3 + NF * UM_S, "small trials staging buffer");
-template <int LM, int UM, int UB>
+__device__ inline double pass_b_alpha(const NlpDev& d, int w);
+template <int LM, int UM, int UB, int KM = EV_MAXK>
 __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d) {
     if (d.lcount && blockIdx.y >= *d.lcount) return;
     const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
     const WorldState& S = d.ws[w];
-    if (!(S.status == 0 && S.searching)) return;
+    if (!(S.status == 0 && (d.b_in_cs || S.searching))) return;
     const RobotParams& rp = *d.rp;
     const int tid = threadIdx.x, K = d.K;
     const long jt = (long)w * d.T + t;
     const int NJ = d.NJ, O = d.O, NP = NJ * O;
     const long nt = d.nt;
-    __shared__ double xk[EV_MAXK][NF];
-    __shared__ double ptab[EV_MAXK][NF][4];  // x_j^g of trial k (the value slices' factors)
-    __shared__ double lck[EV_MAXK][MAX_J][3];
+    __shared__ double xk[KM][NF];
+    __shared__ double ptab[KM][NF][4];  // x_j^g of trial k (the value slices' factors)
+    __shared__ double lck[KM][MAX_J][3];
     __shared__ uint16_t lh[MAX_J][LM];
     __shared__ uint16_t th[NF][UM];
     __shared__ double ubuf[UB];
@@ -1146,7 +1147,7 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     auto tco = reinterpret_cast<double (*)[UM]>(ubuf + MAX_J * LM * 3);
     if (tid < K * NF) {
         const int kk = tid / NF, j = tid % NF;
-        double a = S.alpha;
+        double a = d.b_in_cs ? pass_b_alpha(d, w) : S.alpha;
         for (int q = 0; q < kk; q++) a *= 0.5;
         const double xj = S.x[j] + a * S.dx[j];
         xk[kk][j] = xj;
@@ -1296,6 +1297,9 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     }
 }
 __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) { eval_trials_body<CAP_LM, CAP_UM, UB_FULL>(d); }
+// the sync-free tail's single line-search round: all max_ls trials (K = EV_MAXK + 1) of the few
+// running worlds, round 0's trial included (ipm_world_Cs_all); K * NJ * O <= UB_FULL (host check)
+__global__ __launch_bounds__(EVAL_THREADS) void eval_trials_all(NlpDev d) { eval_trials_body<CAP_LM, CAP_UM, UB_FULL, EV_MAXK + 1>(d); }
 // five waves per SIMD (91 VGPRs): six measured slower (5.5 -> 5.7 ms per solve)
 __global__ __launch_bounds__(EVAL_THREADS) __attribute__((amdgpu_waves_per_eu(5, 5))) void eval_trials_small(NlpDev d) {
     eval_trials_body<LM_S, UM_S, UB_TS>(d);
@@ -1724,9 +1728,9 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     block_reduce_n(v, kinds, lds, out);
 }
 
-__global__ __launch_bounds__(64) void ipm_world_B(NlpDev d) {
-    if (d.lcount && blockIdx.x >= *d.lcount) return;
-    const int w = world_of(d, blockIdx.x);
+// pass B's world step: step sizes, line-search ingredients, the first trial point (every lane of
+// the wave calls it; ipm_world_B, or ipm_world_Cs_all in the sync-free tail)
+__device__ inline void world_B_body(const NlpDev& d, int w) {
     WorldState& S = d.ws[w];
     if (S.status != 0) return;
     double P[19], init[19];
@@ -1755,6 +1759,26 @@ __global__ __launch_bounds__(64) void ipm_world_B(NlpDev d) {
     S.ls = 0;
     S.ftype = 0;
     S.accepted_ok = 0;
+}
+__global__ __launch_bounds__(64) void ipm_world_B(NlpDev d) {
+    if (d.lcount && blockIdx.x >= *d.lcount) return;
+    world_B_body(d, world_of(d, blockIdx.x));
+}
+// the first trial's step alpha = S.ap as world_B_body forms it: pass B's block partials of the
+// primal fraction to the boundary, min onto 1 in block order (world_partials' arithmetic), for the
+// tail's trial passes that run before the world step (NlpDev::b_in_cs)
+__device__ inline double pass_b_alpha(const NlpDev& d, int w) {
+    const double* in = d.partial + (long)w * d.nblk * KA;
+    double a = 1.0;
+    for (int b0 = 0; b0 < d.nblk; b0 += 16) {
+        double x[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) x[u] = in[(long)min(b0 + u, d.nblk - 1) * KA];
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (b0 + u < d.nblk) a = fmin(a, x[u]);
+    }
+    return a;
 }
 
 // pass C: barrier objective and constraint violation at the trial point
@@ -1860,6 +1884,7 @@ __global__ __launch_bounds__(64) void ipm_world_C(NlpDev d) {
         if (d.ls0) d.flags[0] = (int)nrun;
         if (d.ls0 && d.lrun_out) *d.lrun_out = nrun;
         if (d.ls0 && d.nrun_flag) *d.nrun_flag = (int)nrun;
+        if (d.ls0 && d.bt_flag) *d.bt_flag = (int)nsearch;
         d.flags[1] = (int)nsearch;
         if (d.lcount_out) *d.lcount_out = nsearch;
         d.cnt[0] = 0;
@@ -1876,9 +1901,9 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
     if (d.lcount && (unsigned)i >= *d.lcount) return;
     const int w = d.wl[i];
     const WorldState& S = d.ws[w];
-    if (!(S.status == 0 && S.searching)) return;
+    if (!(S.status == 0 && (d.b_in_cs || S.searching))) return;
     __shared__ double lds[(ROW_THREADS / 64) * NA];
-    double alpha = S.alpha;
+    double alpha = d.b_in_cs ? pass_b_alpha(d, w) : S.alpha;
     for (int q = 0; q < k; q++) alpha *= 0.5;
     const double* G = d.gs + (long)blockIdx.y * d.m;
     double logt = 0, rpt = 0;
@@ -1901,9 +1926,46 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
 // (ipm_world_C): the first acceptable one ends the search, or the last (forced) one
 // list entry blockIdx.x (one wave): every trial's two partial sums at once (lane 2 k + q, block
 // partials summed in order as world_partials_at), then the acceptance tests in trial order on lane 0
+__device__ inline void world_Cs_body(const NlpDev& d, int i);
 __global__ __launch_bounds__(64) void ipm_world_Cs(NlpDev d) {
     if (d.lcount && blockIdx.x >= *d.lcount) return;
-    const int i = blockIdx.x, w = d.wl[i];
+    world_Cs_body(d, blockIdx.x);
+}
+// The tail's whole line search in one round (planner.hip run_solver, sync-free tail): every trial
+// k = 0 .. max_ls - 1 of every running world was evaluated values-only (eval_trials_kernel with
+// K = max_ls) and summed (ipm_rows_Cs), so this is round 0 and every later round of
+// ipm_world_C's sequential search at once: the acceptance tests in trial order (world_Cs_body),
+// then round 0's bookkeeping — the worlds still running appended to the next iteration's list, the
+// last block publishing the count as ipm_world_C does for ls0. The chosen trial is then evaluated in
+// full (eval_kernel_t mode 5).
+__global__ __launch_bounds__(64) void ipm_world_Cs_all(NlpDev d) {
+    const bool valid = !d.lcount || blockIdx.x < *d.lcount;
+    const int w = valid ? d.wl[blockIdx.x] : 0;
+    if (valid) {
+        if (d.b_in_cs) world_B_body(d, w);  // lane 0 writes what lane 0 alone reads below
+        world_Cs_body(d, blockIdx.x);
+    }
+    if (threadIdx.x != 0) return;
+    if (valid && d.ws[w].status == 0) {
+        d.wl_run[atomicAdd(&d.cnt[0], 1u)] = w;
+        if (d.ws[w].spec_k > 0) atomicAdd(&d.cnt[1], 1u);  // searched past round 0
+    }
+    __threadfence();
+    if (atomicAdd(&d.cnt[2], 1u) == gridDim.x - 1) {
+        __threadfence();
+        const unsigned nrun = atomicAdd(&d.cnt[0], 0u), nbt = atomicAdd(&d.cnt[1], 0u);
+        d.flags[0] = (int)nrun;
+        d.flags[1] = 0;
+        if (d.lrun_out) *d.lrun_out = nrun;
+        if (d.nrun_flag) *d.nrun_flag = (int)nrun;
+        if (d.bt_flag) *d.bt_flag = (int)nbt;
+        d.cnt[0] = 0;
+        d.cnt[1] = 0;
+        d.cnt[2] = 0;
+    }
+}
+__device__ inline void world_Cs_body(const NlpDev& d, int i) {
+    const int w = d.wl[i];
     WorldState& S = d.ws[w];
     const int lane = threadIdx.x & 63;
     double s = 0.0;

@@ -108,6 +108,8 @@ struct armour_planner {
     int* h_flags = nullptr;   // pinned host, mapped (NlpDev::flags)
     int* d_lists = nullptr;   // [4][max_worlds] active-world lists of the solver
     bool spec = true;         // speculative line-search rounds (ARMOUR_NO_SPEC: sequential only)
+    bool spec_all = true;     // the sync-free tail's one-round line search (eval_trials_all, ipm_world_Cs_all)
+    int tail_search = 1;      // its use (ARMOUR_TAIL_SEARCH): 0 rounds only, 1 adaptive, 2 always
     WorldState* h_ws = nullptr;
     double* h_f = nullptr;
     int* h_feas = nullptr;
@@ -195,6 +197,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     for (int i = 0; i < 6; i++) HIPCK(hipEventCreate(&p->ev[i]));
     for (int i = 0; i < 2; i++) HIPCK(hipEventCreateWithFlags(&p->tev[i], hipEventDisableTiming));
     if (const char* e = std::getenv("ARMOUR_TAIL_WORLDS")) p->tail_worlds = std::atoi(e);
+    if (const char* e = std::getenv("ARMOUR_TAIL_SEARCH"))
+        p->tail_search = !std::strcmp(e, "rounds") ? 0 : !std::strcmp(e, "one") ? 2 : 1;
     const int T = p->T, NJ = p->NJ, Om = p->Omax > 0 ? p->Omax : 1, Wm = p->Wmax;
     int rc = 0;
     if ((rc = p->alloc(&p->d_rp, 1))) return rc;
@@ -435,7 +439,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         return rc;
     // the solver's two continue flags live in mapped host memory: kernels store 1 into them, the
     // host clears and reads them between synchronised rounds (no fill or copy per round)
-    HIPCK(hipHostMalloc((void**)&p->h_flags, 4 * sizeof(int), hipHostMallocMapped));
+    HIPCK(hipHostMalloc((void**)&p->h_flags, 6 * sizeof(int), hipHostMallocMapped));
     HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
     // active-world lists: two per iteration (ping-pong), two per line-search round
     if ((rc = p->alloc(&p->d_lists, 4 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 12))) return rc;
@@ -451,13 +455,19 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // round reads the plane cache (ARMOUR planner, fp64); otherwise the rounds run one by one.
     d.K = d.opt.max_ls - 1;
     p->spec = !std::getenv("ARMOUR_NO_SPEC") && d.K > 0 && d.K <= EV_MAXK && d.pcache && !p->armtd && !p->eval_f32;
+    // The sync-free tail may search all max_ls trials of its (at most tail_worlds) running worlds in
+    // one round (run_solver)
+    p->spec_all = p->spec && p->tail_search > 0 && (d.K + 1) * NJ * Om <= UB_FULL;
     if (p->spec) {
-        const size_t ns = (size_t)Wm * d.K;
+        const size_t nall = p->spec_all ? (size_t)std::min(Wm, std::max(p->tail_worlds, 0)) * (d.K + 1) : 0;
+        const size_t ns = std::max((size_t)Wm * d.K, nall);
         if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.fs, ns)) || (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
             return rc;
     }
     HIPCK(hipMemset(d.cnt, 0, 12 * sizeof(unsigned)));
     d.lcount = nullptr;
+    d.b_in_cs = 0;
+    d.bt_flag = nullptr;
     d.lrun_out = nullptr;
     d.nrun_flag = nullptr;
     d.lcount_out = nullptr;
@@ -732,6 +742,12 @@ static int run_solver(armour_planner* p) {
     // world's arithmetic is that of the synchronised loop.
     int cur = 0, nrun = W;
     bool tail = false;       // iteration it - 1 ran sync-free (its running count not yet read)
+    // worlds that backtracked (searched past round 0) in the latest iteration the host knows of: the
+    // tail takes the one-round search while they do (ARMOUR_TAIL_SEARCH=adaptive). A converging
+    // world mostly accepts round 0's trial, which its own full evaluation serves faster than the
+    // values of every trial plus the chosen one's full evaluation; a backtracking world saves a
+    // round. The choice changes launches only, never a world's arithmetic.
+    int backtracked = W;
     for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
         const bool tl = it > 0 && p->spec && d.pcready && nrun <= p->tail_worlds;
         NlpDev di = d;
@@ -746,8 +762,42 @@ static int run_solver(armour_planner* p) {
             hipLaunchKernelGGL(ipm_rows_DA, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
             hipLaunchKernelGGL(ipm_world_DA, dim3(nrun), dim3(64), 0, p->stream, di, ns);
         }
+        const bool one = tl && p->spec_all && (p->tail_search == 2 || backtracked > 0);
         hipLaunchKernelGGL(ipm_rows_B, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
-        hipLaunchKernelGGL(ipm_world_B, dim3(nrun), dim3(64), 0, p->stream, di);
+        if (!one) hipLaunchKernelGGL(ipm_world_B, dim3(nrun), dim3(64), 0, p->stream, di);
+        if (one) {
+            // The tail's line search in one round: the values of all max_ls trials of every running
+            // world at once (round 0's included, the step taken from pass B's partials), then pass
+            // B's world step, the acceptance tests in trial order and round 0's running list and
+            // counts (ipm_world_Cs_all), then the chosen trial in full. Four launches where pass B's
+            // world step and round 0 took four and the speculative round four more; the tests, and
+            // so the plans, are those of sequential rounds.
+            NlpDev ds = d;
+            ds.K = d.K + 1;
+            ds.b_in_cs = 1;  // pass B's world step in ipm_world_Cs_all
+            ds.wl = Li[cur];
+            ds.wl_run = Li[1 - cur];
+            ds.lcount = di.lcount;
+            ds.lrun_out = d.cnt + 8 + ((it + 1) & 1);
+            ds.nrun_flag = d.flags + 2 + (it & 1);
+            ds.bt_flag = d.flags + 4 + (it & 1);
+            hipLaunchKernelGGL(eval_trials_all, dim3(p->T, nrun), dim3(EVAL_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * ds.K), dim3(ROW_THREADS), 0, p->stream, ds);
+            hipLaunchKernelGGL(ipm_world_Cs_all, dim3(nrun), dim3(64), 0, p->stream, ds);
+            launch_eval(p, dim3(p->T, nrun), ds, 5);
+            HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
+            HIPCK(hipGetLastError());
+            cur = 1 - cur;
+            if (tail) {
+                HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
+                const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
+                backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
+                if (prev == 0) break;
+                nrun = prev < nrun ? prev : nrun;
+            }
+            tail = true;
+            continue;
+        }
         // Round 0 of the line search for every running world, then one host synchronisation. The
         // worlds still searching after it (the tail of the backtracking) run the remaining rounds
         // without one: a few of them all remaining trials at once (speculative round, ipm_world_Cs),
@@ -765,6 +815,7 @@ static int run_solver(armour_planner* p) {
             if (tl) {
                 dc.lcount = di.lcount;
                 dc.nrun_flag = d.flags + 2 + (it & 1);
+                dc.bt_flag = d.flags + 4 + (it & 1);
             }
             launch_eval(p, dim3(p->T, nrun), dc, 1);
             hipLaunchKernelGGL(ipm_rows_C, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, dc);
@@ -773,6 +824,7 @@ static int run_solver(armour_planner* p) {
                 HIPCK(hipStreamSynchronize(p->stream));
                 nnext = ((volatile int*)p->h_flags)[0];
                 nsearch = ((volatile int*)p->h_flags)[1];
+                backtracked = nsearch;
             }
         }
         if (tl) {
@@ -794,6 +846,7 @@ static int run_solver(armour_planner* p) {
                 // iteration it - 1's running count: the worlds iteration it was launched for
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
+                backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;  // iteration it had nothing to do
                 nrun = prev < nrun ? prev : nrun;
             }

@@ -116,12 +116,15 @@ def test_speculative_line_search_matches_sequential():
         assert np.array_equal(g_s[w], Q.constraints(w)) and np.array_equal(c_s[w], Q.link_centers(w))
 
 
+@pytest.mark.parametrize("search", ["adaptive", "one", "rounds"])
 @pytest.mark.parametrize("tail", ["1000", "16"])
-def test_sync_free_tail_matches_synchronised(tail):
+def test_sync_free_tail_matches_synchronised(tail, search):
     """Sync-free tail iterations (planner.hip run_solver: bounded grids, device-side list lengths,
     the running count read one iteration later) give bitwise the plans of the loop synchronised
     every iteration (ARMOUR_TAIL_WORLDS=0). "1000" runs every iteration after the first sync-free;
-    also one world alone, the drop-in's batch."""
+    also one world alone, the drop-in's batch. The tail's line search runs in one round of all
+    trials (eval_trials_all, ipm_world_Cs_all: "one"), round by round ("rounds"), or picked per
+    iteration by whether worlds backtracked ("adaptive", the default)."""
     import os
 
     T, O = 40, 10
@@ -129,10 +132,12 @@ def test_sync_free_tail_matches_synchronised(tail):
         planners = []
         for tw in ("0", tail):
             os.environ["ARMOUR_TAIL_WORLDS"] = tw
+            os.environ["ARMOUR_TAIL_SEARCH"] = search
             try:
                 planners.append(A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds)))
             finally:
                 del os.environ["ARMOUR_TAIL_WORLDS"]
+                del os.environ["ARMOUR_TAIL_SEARCH"]
         (res_s, _), (res_t, _) = [P.plan(worlds) for P in planners]
         for w, (a, b) in enumerate(zip(res_s, res_t)):
             assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"]
