@@ -1584,11 +1584,26 @@ __device__ inline void world_partials_at(const double* base, int nblk, int strid
     }
 }
 
-__device__ inline void world_A_body(const NlpDev& d, int w, int nside);
-__global__ __launch_bounds__(64) void ipm_world_A(NlpDev d, int nside) { world_A_body(d, world_of(d, blockIdx.x), nside); }
+__device__ inline void world_A_body(const NlpDev& d, WorldState& S, int w, int nside);
+// A world kernel (one wave) works on its world's state staged in LDS: one coalesced round trip in
+// and one out, where lane 0's steps would otherwise wait on a dependent global load per field
+__device__ inline void ws_copy(WorldState& dst, const WorldState& src) {
+    static_assert(sizeof(WorldState) % 8 == 0, "WorldState in 8-byte words");
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(&src);
+    uint64_t* t = reinterpret_cast<uint64_t*>(&dst);
+    for (int k = threadIdx.x; k < (int)(sizeof(WorldState) / 8); k += blockDim.x) t[k] = s[k];
+}
+__global__ __launch_bounds__(64) void ipm_world_A(NlpDev d, int nside) {
+    const int w = world_of(d, blockIdx.x);
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    world_A_body(d, S, w, nside);
+    __syncthreads();
+    ws_copy(d.ws[w], S);
+}
 // pass A's world step: convergence test, barrier update, Newton step; every lane of the wave calls it
-__device__ inline void world_A_body(const NlpDev& d, int w, int nside) {
-    WorldState& S = d.ws[w];
+__device__ inline void world_A_body(const NlpDev& d, WorldState& S, int w, int nside) {
     if (S.status != 0) return;
     if (S.iter >= d.opt.max_iter) {  // oracle: loop ends without a final check
         if (threadIdx.x == 0) S.status = 2;
@@ -1730,8 +1745,7 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
 
 // pass B's world step: step sizes, line-search ingredients, the first trial point (every lane of
 // the wave calls it; ipm_world_B, or ipm_world_Cs_all in the sync-free tail)
-__device__ inline void world_B_body(const NlpDev& d, int w) {
-    WorldState& S = d.ws[w];
+__device__ inline void world_B_body(const NlpDev& d, WorldState& S, int w) {
     if (S.status != 0) return;
     double P[19], init[19];
     int op[19];
@@ -1762,7 +1776,13 @@ __device__ inline void world_B_body(const NlpDev& d, int w) {
 }
 __global__ __launch_bounds__(64) void ipm_world_B(NlpDev d) {
     if (d.lcount && blockIdx.x >= *d.lcount) return;
-    world_B_body(d, world_of(d, blockIdx.x));
+    const int w = world_of(d, blockIdx.x);
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    world_B_body(d, S, w);
+    __syncthreads();
+    ws_copy(d.ws[w], S);
 }
 // the first trial's step alpha = S.ap as world_B_body forms it: pass B's block partials of the
 // primal fraction to the boundary, min onto 1 in block order (world_partials' arithmetic), for the
@@ -1813,8 +1833,7 @@ __device__ inline bool filter_pass(const WorldState& S, double thetat, double ph
     const bool fail = q < S.nfilt && !(thetat < S.filt_theta[q] || phit < S.filt_phi[q]);
     return __ballot(fail) == 0;
 }
-__device__ inline void world_C_body(const NlpDev& d, int w) {
-    WorldState& S = d.ws[w];
+__device__ inline void world_C_body(const NlpDev& d, WorldState& S, int w) {
     if (!(S.status == 0 && S.searching)) return;
     double P[2];
     const double init[2] = {0.0, 0.0};
@@ -1870,9 +1889,15 @@ __device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt,
 __global__ __launch_bounds__(64) void ipm_world_C(NlpDev d) {
     const bool valid = !d.lcount || blockIdx.x < *d.lcount;
     const int w = valid ? world_of(d, blockIdx.x) : 0;
-    if (valid) world_C_body(d, w);
+    __shared__ WorldState S;
+    if (valid) {
+        ws_copy(S, d.ws[w]);
+        __syncthreads();
+        world_C_body(d, S, w);
+        __syncthreads();
+        ws_copy(d.ws[w], S);
+    }
     if (threadIdx.x != 0) return;
-    const WorldState& S = d.ws[w];
     if (valid && S.status == 0) {
         if (d.ls0) d.wl_run[atomicAdd(&d.cnt[0], 1u)] = w;
         if (S.searching) d.wl_search[atomicAdd(&d.cnt[1], 1u)] = w;
@@ -1926,10 +1951,16 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
 // (ipm_world_C): the first acceptable one ends the search, or the last (forced) one
 // list entry blockIdx.x (one wave): every trial's two partial sums at once (lane 2 k + q, block
 // partials summed in order as world_partials_at), then the acceptance tests in trial order on lane 0
-__device__ inline void world_Cs_body(const NlpDev& d, int i);
+__device__ inline void world_Cs_body(const NlpDev& d, WorldState& S, int i);
 __global__ __launch_bounds__(64) void ipm_world_Cs(NlpDev d) {
     if (d.lcount && blockIdx.x >= *d.lcount) return;
-    world_Cs_body(d, blockIdx.x);
+    const int w = d.wl[blockIdx.x];
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    world_Cs_body(d, S, blockIdx.x);
+    __syncthreads();
+    ws_copy(d.ws[w], S);
 }
 // The tail's whole line search in one round (planner.hip run_solver, sync-free tail): every trial
 // k = 0 .. max_ls - 1 of every running world was evaluated values-only (eval_trials_kernel with
@@ -1941,14 +1972,19 @@ __global__ __launch_bounds__(64) void ipm_world_Cs(NlpDev d) {
 __global__ __launch_bounds__(64) void ipm_world_Cs_all(NlpDev d) {
     const bool valid = !d.lcount || blockIdx.x < *d.lcount;
     const int w = valid ? d.wl[blockIdx.x] : 0;
+    __shared__ WorldState S;
     if (valid) {
-        if (d.b_in_cs) world_B_body(d, w);  // lane 0 writes what lane 0 alone reads below
-        world_Cs_body(d, blockIdx.x);
+        ws_copy(S, d.ws[w]);
+        __syncthreads();
+        if (d.b_in_cs) world_B_body(d, S, w);  // lane 0 writes what lane 0 alone reads below
+        world_Cs_body(d, S, blockIdx.x);
+        __syncthreads();
+        ws_copy(d.ws[w], S);
     }
     if (threadIdx.x != 0) return;
-    if (valid && d.ws[w].status == 0) {
+    if (valid && S.status == 0) {
         d.wl_run[atomicAdd(&d.cnt[0], 1u)] = w;
-        if (d.ws[w].spec_k > 0) atomicAdd(&d.cnt[1], 1u);  // searched past round 0
+        if (S.spec_k > 0) atomicAdd(&d.cnt[1], 1u);  // searched past round 0
     }
     __threadfence();
     if (atomicAdd(&d.cnt[2], 1u) == gridDim.x - 1) {
@@ -1964,9 +2000,7 @@ __global__ __launch_bounds__(64) void ipm_world_Cs_all(NlpDev d) {
         d.cnt[2] = 0;
     }
 }
-__device__ inline void world_Cs_body(const NlpDev& d, int i) {
-    const int w = d.wl[i];
-    WorldState& S = d.ws[w];
+__device__ inline void world_Cs_body(const NlpDev& d, WorldState& S, int i) {
     const int lane = threadIdx.x & 63;
     double s = 0.0;
     if (lane < 2 * d.K) {
@@ -2027,8 +2061,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
 }
 
 // pass D's world step: BFGS update, accept the trial point; every lane of the wave calls it
-__device__ inline void world_D_body(const NlpDev& d, int w) {
-    WorldState& S = d.ws[w];
+__device__ inline void world_D_body(const NlpDev& d, WorldState& S, int w) {
     if (S.status != 0) return;
     double wn[NF];
     const double init[NF] = {};
@@ -2072,15 +2105,27 @@ __device__ inline void world_D_body(const NlpDev& d, int w) {
     S.iter++;
     if (S.nfail >= 3) S.status = 3;
 }
-__global__ __launch_bounds__(64) void ipm_world_D(NlpDev d) { world_D_body(d, world_of(d, blockIdx.x)); }
-__device__ inline void world_A_body(const NlpDev& d, int w, int nside);
+__global__ __launch_bounds__(64) void ipm_world_D(NlpDev d) {
+    const int w = world_of(d, blockIdx.x);
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    world_D_body(d, S, w);
+    __syncthreads();
+    ws_copy(d.ws[w], S);
+}
 // the fused passes' world step: D's (of the previous iteration), then A's, one wave
 __global__ __launch_bounds__(64) void ipm_world_DA(NlpDev d, int nside) {
     if (d.lcount && blockIdx.x >= *d.lcount) return;
     const int w = world_of(d, blockIdx.x);
-    world_D_body(d, w);
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    world_D_body(d, S, w);
     __syncthreads();  // lane 0's WorldState stores before every lane's reads in world_A_body
-    world_A_body(d, w, nside);
+    world_A_body(d, S, w, nside);
+    __syncthreads();
+    ws_copy(d.ws[w], S);
 }
 
 // finalize_solution's feasibility re-check (NLPclass.cu:449-538): one block per world
