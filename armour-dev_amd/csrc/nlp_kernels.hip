@@ -64,6 +64,23 @@ __device__ inline void row_bounds(const NlpDev& d, long i, int r, double& L, dou
     L = col ? -1e19 : d.L[i];
     U = col ? 0.0 : d.U[i];
 }
+// The row passes read a row's state in one batch before its arithmetic: the slack and multiplier
+// slots of both sides exist for every row (zero where a side is absent) and are read
+// unconditionally, and a collision row's bounds load comes from one cached word of its world
+// (wb = w * R) instead of the row's own slot. A row then waits for memory once; loads behind each
+// side's branch and re-reads after each store had waited a round trip apiece (~6 per row).
+struct RowBounds {
+    double Lm, Um;
+    bool col;
+    __device__ RowBounds(const NlpDev& d, long i, long wb, int r) {
+        col = r >= d.nt && r < d.nt + d.T * d.NJ * d.O;
+        const long ib = col ? wb : i;
+        Lm = d.L[ib];
+        Um = d.U[ib];
+    }
+    __device__ double L() const { return col ? -1e19 : Lm; }
+    __device__ double U() const { return col ? 0.0 : Um; }
+};
 __device__ inline bool has_lo(const NlpDev& d, double L) { return L > -d.opt.inf_bound; }
 __device__ inline bool has_hi(const NlpDev& d, double U) { return U < d.opt.inf_bound; }
 
@@ -71,6 +88,10 @@ __device__ inline bool has_hi(const NlpDev& d, double U) { return U < d.opt.inf_
 // gradient is n . dc/dx from the compact form (bitwise the value eval_kernel forms densely)
 __device__ inline double row_va(const NlpDev& d, int slot, int w, int r, const double* x, double* a) {
     const int nc = d.T * d.NJ * d.O;
+    // the value's load ahead of the branches (a box row's, from row 0, goes unused), so that it
+    // travels with the row's other loads instead of after them
+    const long gi = gidx(d, slot, w, r < d.m ? r : 0);
+    const double v = d.g[gi];
     if (r >= d.nt && r < d.nt + nc) {
         const int q = r - d.nt, lt = q / d.O, l = lt / d.T, t = lt % d.T;
         const double* n = d.jn + slot * d.njn + ((long)w * nc + q) * 3;
@@ -78,14 +99,13 @@ __device__ inline double row_va(const NlpDev& d, int slot, int w, int r, const d
         const double n0 = n[0], n1 = n[1], n2 = n[2];
 #pragma unroll
         for (int j = 0; j < NF; j++) a[j] = n0 * D[3 * j] + n1 * D[3 * j + 1] + n2 * D[3 * j + 2];
-        return d.g[gidx(d, slot, w, r)];
+        return v;
     }
     if (r < d.m) {
-        const long gi = gidx(d, slot, w, r);
         const double* J = d.J + gi * NF;
 #pragma unroll
         for (int j = 0; j < NF; j++) a[j] = J[j];
-        return d.g[gi];
+        return v;
     }
 #pragma unroll
     for (int j = 0; j < NF; j++) a[j] = (j == r - d.m) ? 1.0 : 0.0;
@@ -1381,11 +1401,13 @@ struct AAcc {
         sumc = 0; minc = 1e300;
     }
 };
-__device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, long i, double v, const double* a, double L,
-                                                            double U, double mu, AAcc& c) {
+// pass A's row accumulation with the row's slacks and multipliers given (registers)
+__device__ inline __attribute__((always_inline)) void row_A_sz(const NlpDev& d, long i, double v, const double* a, double L,
+                                                               double U, double mu, double slo, double zlo, double shi,
+                                                               double zhi, AAcc& c) {
     double wr = 0, sig = 0, c1 = 0, c2 = 0;
     if (has_lo(d, L)) {
-        const double s = d.slo[i], z = d.zlo[i];
+        const double s = slo, z = zlo;
         const double rp = (v - L) - s;
         d.rplo[i] = rp;
         wr += z;
@@ -1401,7 +1423,7 @@ __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, lon
         c2 += sg * rp;
     }
     if (has_hi(d, U)) {
-        const double s = d.shi[i], z = d.zhi[i];
+        const double s = shi, z = zhi;
         const double rp = (U - v) - s;
         d.rphi[i] = rp;
         wr -= z;
@@ -1425,6 +1447,10 @@ __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, lon
 #pragma unroll
         for (int q = p; q < NF; q++) c.M[k++] += sig * a[p] * a[q];
     }
+}
+__device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, long i, double v, const double* a, double L,
+                                                            double U, double mu, AAcc& c) {
+    row_A_sz(d, i, v, a, L, U, mu, d.slo[i], d.zlo[i], d.shi[i], d.zhi[i], c);
 }
 constexpr int NA = 55;  // pass A's partial sums per row block (<= KA)
 static_assert(NA <= KA, "pass A partials fit the partial slots");
@@ -1500,15 +1526,38 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
     for (int j = 0; j < NF; j++) wn[j] = 0;
     AAcc c;
     c.zero();
-    const long r0 = (long)blockIdx.x * d.chunk;
+    const double ks = d.opt.kappa_sigma;
+    const long r0 = (long)blockIdx.x * d.chunk, wb = (long)w * d.R;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        // the row's loads in one batch, then row_D's and row_A's arithmetic on registers (A reads
+        // the slacks and multipliers D has just formed)
+        const long i = wb + r;
+        const RowBounds B(d, i, wb, (int)r);
+        const double slo = d.slo[i], zlo = d.zlo[i], dslo = d.dslo[i], dzlo = d.dzlo[i];
+        const double shi = d.shi[i], zhi = d.zhi[i], dshi = d.dshi[i], dzhi = d.dzhi[i];
         double a[NF];
         const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
-        const long i = (long)w * d.R + r;
-        double L, U;
-        row_bounds(d, i, (int)r, L, U);
-        row_D(d, i, a, L, U, mu, ad, alpha, wn);
-        row_A(d, i, v, a, L, U, mu, c);
+        const double L = B.L(), U = B.U();
+        double wv = 0, sl = slo, zl = zlo, sh = shi, zh = zhi;
+        if (has_lo(d, L)) {
+            const double zn = zlo + ad * dzlo;
+            wv += zn;
+            sl = slo + alpha * dslo;
+            zl = fmin(fmax(zn, mu / (ks * sl)), ks * mu / sl);
+            d.slo[i] = sl;
+            d.zlo[i] = zl;
+        }
+        if (has_hi(d, U)) {
+            const double zn = zhi + ad * dzhi;
+            wv -= zn;
+            sh = shi + alpha * dshi;
+            zh = fmin(fmax(zn, mu / (ks * sh)), ks * mu / sh);
+            d.shi[i] = sh;
+            d.zhi[i] = zh;
+        }
+#pragma unroll
+        for (int j = 0; j < NF; j++) wn[j] += wv * a[j];
+        row_A_sz(d, i, v, a, L, U, mu, sl, zl, sh, zh, c);
     }
     const int kinds[NF] = {};
     block_reduce_n(wn, kinds, lds, d.partial2 + ((long)w * d.nblk + blockIdx.x) * KA2);
@@ -1698,35 +1747,40 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     double ap = 1.0, ad = 1.0, rp1 = 0, bdir = 0, logs = 0, wa[NF], wb[NF];
 #pragma unroll
     for (int j = 0; j < NF; j++) { wa[j] = 0; wb[j] = 0; }
-    const long r0 = (long)blockIdx.x * d.chunk;
+    double dx[NF];
+#pragma unroll
+    for (int j = 0; j < NF; j++) dx[j] = S.dx[j];
+    const long r0 = (long)blockIdx.x * d.chunk, w0 = (long)w * d.R;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        const long i = w0 + r;  // the row's loads in one batch (RowBounds)
+        const RowBounds B(d, i, w0, (int)r);
+        const double slo = d.slo[i], zlo = d.zlo[i], rplo = d.rplo[i];
+        const double shi = d.shi[i], zhi = d.zhi[i], rphi = d.rphi[i];
         double a[NF];
         row_va(d, S.cur, w, (int)r, S.x, a);
         double adx = 0;
 #pragma unroll
-        for (int j = 0; j < NF; j++) adx += a[j] * S.dx[j];
-        const long i = (long)w * d.R + r;
-        double L, U;
-        row_bounds(d, i, (int)r, L, U);
+        for (int j = 0; j < NF; j++) adx += a[j] * dx[j];
+        const double L = B.L(), U = B.U();
         double za = 0, zb = 0;
         if (has_lo(d, L)) {
-            const double s = d.slo[i], z = d.zlo[i], sg = z / s;
-            const double ds = adx + d.rplo[i];
+            const double s = slo, z = zlo, sg = z / s;
+            const double ds = adx + rplo;
             const double dz = mu / s - z - sg * ds;
             d.dslo[i] = ds; d.dzlo[i] = dz;
             if (ds < 0) ap = fmin(ap, -tau * s / ds);
             if (dz < 0) ad = fmin(ad, -tau * z / dz);
-            rp1 += fabs(d.rplo[i]); bdir += ds / s; logs += log(s);
+            rp1 += fabs(rplo); bdir += ds / s; logs += log(s);
             za += z; zb += dz;
         }
         if (has_hi(d, U)) {
-            const double s = d.shi[i], z = d.zhi[i], sg = z / s;
-            const double ds = -adx + d.rphi[i];
+            const double s = shi, z = zhi, sg = z / s;
+            const double ds = -adx + rphi;
             const double dz = mu / s - z - sg * ds;
             d.dshi[i] = ds; d.dzhi[i] = dz;
             if (ds < 0) ap = fmin(ap, -tau * s / ds);
             if (dz < 0) ad = fmin(ad, -tau * z / dz);
-            rp1 += fabs(d.rphi[i]); bdir += ds / s; logs += log(s);
+            rp1 += fabs(rphi); bdir += ds / s; logs += log(s);
             za -= z; zb -= dz;
         }
 #pragma unroll
@@ -1809,15 +1863,17 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
     if (!(S.status == 0 && S.searching)) return;
     __shared__ double lds[(ROW_THREADS / 64) * NA];
     double logt = 0, rpt = 0;
-    const long r0 = (long)blockIdx.x * d.chunk;
+    const double alpha = S.alpha;
+    const long r0 = (long)blockIdx.x * d.chunk, wb = (long)w * d.R;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        const long i = wb + r;  // the row's loads in one batch (RowBounds)
+        const RowBounds B(d, i, wb, (int)r);
+        const double slo = d.slo[i], dslo = d.dslo[i], shi = d.shi[i], dshi = d.dshi[i];
         double a[NF];
         const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
-        const long i = (long)w * d.R + r;
-        double L, U;
-        row_bounds(d, i, (int)r, L, U);
-        if (has_lo(d, L)) { const double st = d.slo[i] + S.alpha * d.dslo[i]; logt += log(st); rpt += fabs((v - L) - st); }
-        if (has_hi(d, U)) { const double st = d.shi[i] + S.alpha * d.dshi[i]; logt += log(st); rpt += fabs((U - v) - st); }
+        const double L = B.L(), U = B.U();
+        if (has_lo(d, L)) { const double st = slo + alpha * dslo; logt += log(st); rpt += fabs((v - L) - st); }
+        if (has_hi(d, U)) { const double st = shi + alpha * dshi; logt += log(st); rpt += fabs((U - v) - st); }
     }
     double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
     double v[2] = {logt, rpt};
@@ -1932,14 +1988,15 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
     for (int q = 0; q < k; q++) alpha *= 0.5;
     const double* G = d.gs + (long)blockIdx.y * d.m;
     double logt = 0, rpt = 0;
-    const long r0 = (long)blockIdx.x * d.chunk;
+    const long r0 = (long)blockIdx.x * d.chunk, wb = (long)w * d.R;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
+        const long ii = wb + r;  // the row's loads in one batch (RowBounds)
+        const RowBounds B(d, ii, wb, (int)r);
+        const double slo = d.slo[ii], dslo = d.dslo[ii], shi = d.shi[ii], dshi = d.dshi[ii];
         const double v = r < d.m ? G[r] : S.x[r - d.m] + alpha * S.dx[r - d.m];  // box row: the trial's x
-        const long ii = (long)w * d.R + r;
-        double L, U;
-        row_bounds(d, ii, (int)r, L, U);
-        if (has_lo(d, L)) { const double st = d.slo[ii] + alpha * d.dslo[ii]; logt += log(st); rpt += fabs((v - L) - st); }
-        if (has_hi(d, U)) { const double st = d.shi[ii] + alpha * d.dshi[ii]; logt += log(st); rpt += fabs((U - v) - st); }
+        const double L = B.L(), U = B.U();
+        if (has_lo(d, L)) { const double st = slo + alpha * dslo; logt += log(st); rpt += fabs((v - L) - st); }
+        if (has_hi(d, U)) { const double st = shi + alpha * dshi; logt += log(st); rpt += fabs((U - v) - st); }
     }
     double* out = d.partial_s + ((long)blockIdx.y * d.nblk + blockIdx.x) * KA;
     double v[2] = {logt, rpt};
