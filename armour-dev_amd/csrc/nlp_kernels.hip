@@ -69,14 +69,19 @@ __device__ inline void row_bounds(const NlpDev& d, long i, int r, double& L, dou
 // unconditionally, and a collision row's bounds load comes from one cached word of its world
 // (wb = w * R) instead of the row's own slot. A row then waits for memory once; loads behind each
 // side's branch and re-reads after each store had waited a round trip apiece (~6 per row).
+// A collision row has no lower side (L = -1e19): its lower-side slots are read from those of the
+// world's first collision row (lo; unused, and never written by a row pass), one cached word, so
+// the batch costs no bytes for them.
 struct RowBounds {
     double Lm, Um;
     bool col;
+    long lo;  // index of the row's lower-side slots
     __device__ RowBounds(const NlpDev& d, long i, long wb, int r) {
         col = r >= d.nt && r < d.nt + d.T * d.NJ * d.O;
         const long ib = col ? wb : i;
         Lm = d.L[ib];
         Um = d.U[ib];
+        lo = col ? wb + d.nt : i;
     }
     __device__ double L() const { return col ? -1e19 : Lm; }
     __device__ double U() const { return col ? 0.0 : Um; }
@@ -1533,7 +1538,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
         // the slacks and multipliers D has just formed)
         const long i = wb + r;
         const RowBounds B(d, i, wb, (int)r);
-        const double slo = d.slo[i], zlo = d.zlo[i], dslo = d.dslo[i], dzlo = d.dzlo[i];
+        const double slo = d.slo[B.lo], zlo = d.zlo[B.lo], dslo = d.dslo[B.lo], dzlo = d.dzlo[B.lo];
         const double shi = d.shi[i], zhi = d.zhi[i], dshi = d.dshi[i], dzhi = d.dzhi[i];
         double a[NF];
         const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
@@ -1754,7 +1759,7 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
         const long i = w0 + r;  // the row's loads in one batch (RowBounds)
         const RowBounds B(d, i, w0, (int)r);
-        const double slo = d.slo[i], zlo = d.zlo[i], rplo = d.rplo[i];
+        const double slo = d.slo[B.lo], zlo = d.zlo[B.lo], rplo = d.rplo[B.lo];
         const double shi = d.shi[i], zhi = d.zhi[i], rphi = d.rphi[i];
         double a[NF];
         row_va(d, S.cur, w, (int)r, S.x, a);
@@ -1868,7 +1873,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
         const long i = wb + r;  // the row's loads in one batch (RowBounds)
         const RowBounds B(d, i, wb, (int)r);
-        const double slo = d.slo[i], dslo = d.dslo[i], shi = d.shi[i], dshi = d.dshi[i];
+        const double slo = d.slo[B.lo], dslo = d.dslo[B.lo], shi = d.shi[i], dshi = d.dshi[i];
         double a[NF];
         const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
         const double L = B.L(), U = B.U();
@@ -1992,7 +1997,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_Cs(NlpDev d) {
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
         const long ii = wb + r;  // the row's loads in one batch (RowBounds)
         const RowBounds B(d, ii, wb, (int)r);
-        const double slo = d.slo[ii], dslo = d.dslo[ii], shi = d.shi[ii], dshi = d.dshi[ii];
+        const double slo = d.slo[B.lo], dslo = d.dslo[B.lo], shi = d.shi[ii], dshi = d.dshi[ii];
         const double v = r < d.m ? G[r] : S.x[r - d.m] + alpha * S.dx[r - d.m];  // box row: the trial's x
         const double L = B.L(), U = B.U();
         if (has_lo(d, L)) { const double st = slo + alpha * dslo; logt += log(st); rpt += fabs((v - L) - st); }
