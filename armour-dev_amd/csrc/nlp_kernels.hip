@@ -1413,8 +1413,7 @@ __device__ inline __attribute__((always_inline)) void row_A_sz(const NlpDev& d, 
     double wr = 0, sig = 0, c1 = 0, c2 = 0;
     if (has_lo(d, L)) {
         const double s = slo, z = zlo;
-        const double rp = (v - L) - s;
-        d.rplo[i] = rp;
+        const double rp = (v - L) - s;  // (not stored: pass B forms it again from v and s)
         wr += z;
         c.inf_p = fmax(c.inf_p, fabs(rp));
         c.compl0 = fmax(c.compl0, s * z);
@@ -1430,7 +1429,6 @@ __device__ inline __attribute__((always_inline)) void row_A_sz(const NlpDev& d, 
     if (has_hi(d, U)) {
         const double s = shi, z = zhi;
         const double rp = (U - v) - s;
-        d.rphi[i] = rp;
         wr -= z;
         c.inf_p = fmax(c.inf_p, fabs(rp));
         c.compl0 = fmax(c.compl0, s * z);
@@ -1759,14 +1757,17 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
         const long i = w0 + r;  // the row's loads in one batch (RowBounds)
         const RowBounds B(d, i, w0, (int)r);
-        const double slo = d.slo[B.lo], zlo = d.zlo[B.lo], rplo = d.rplo[B.lo];
-        const double shi = d.shi[i], zhi = d.zhi[i], rphi = d.rphi[i];
+        const double slo = d.slo[B.lo], zlo = d.zlo[B.lo];
+        const double shi = d.shi[i], zhi = d.zhi[i];
         double a[NF];
-        row_va(d, S.cur, w, (int)r, S.x, a);
+        const double v = row_va(d, S.cur, w, (int)r, S.x, a);
         double adx = 0;
 #pragma unroll
         for (int j = 0; j < NF; j++) adx += a[j] * dx[j];
         const double L = B.L(), U = B.U();
+        // pass A's primal residuals, formed as row_A_sz forms them (same point, slot and slacks)
+        // instead of stored there and re-read
+        const double rplo = (v - L) - slo, rphi = (U - v) - shi;
         double za = 0, zb = 0;
         if (has_lo(d, L)) {
             const double s = slo, z = zlo, sg = z / s;
