@@ -88,7 +88,7 @@ struct NlpDev {
                             // latest evaluation; region 2 the final iterate's (feasible_kernel)
     long lcs;
     // solver row state [W][R]
-    double *slo, *shi, *zlo, *zhi, *dslo, *dshi, *dzlo, *dzhi;
+    double *slo, *shi, *zlo, *zhi, *dslo, *dshi;
     double* partial;        // [W][nblk][KA]
     double* partial2;       // [W][nblk][KA2]: pass D
     WorldState* ws;         // [W]

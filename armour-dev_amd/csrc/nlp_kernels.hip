@@ -1471,20 +1471,27 @@ __device__ inline void reduce_A(const NlpDev& d, int w, AAcc& c, double* lds) {
     for (int k = 0; k < NA; k++) kinds[k] = (k >= 7 && k <= 9) ? 1 : k == 54 ? 2 : 0;
     block_reduce_n(v, kinds, lds, out);
 }
+// pass B's multiplier step of one side, dz = mu / s - z - (z / s) ds, exactly as ipm_rows_B forms
+// it: pass D forms it again from the same s, z, ds and mu (pass A's barrier update comes after D)
+// instead of storing and re-reading it
+__device__ inline double dual_step(double mu, double s, double z, double ds) {
+    const double sg = z / s;
+    return mu / s - z - sg * ds;
+}
 // pass D's row update (accept the trial: slacks, multipliers) and the BFGS ingredient sum w a
 __device__ inline __attribute__((always_inline)) void row_D(const NlpDev& d, long i, const double* a, double L, double U,
                                                             double mu, double ad, double alpha, double* wn) {
     const double ks = d.opt.kappa_sigma;
     double wv = 0;
     if (has_lo(d, L)) {
-        const double zn = d.zlo[i] + ad * d.dzlo[i];
+        const double zn = d.zlo[i] + ad * dual_step(mu, d.slo[i], d.zlo[i], d.dslo[i]);
         wv += zn;
         const double s = d.slo[i] + alpha * d.dslo[i];
         d.slo[i] = s;
         d.zlo[i] = fmin(fmax(zn, mu / (ks * s)), ks * mu / s);
     }
     if (has_hi(d, U)) {
-        const double zn = d.zhi[i] + ad * d.dzhi[i];
+        const double zn = d.zhi[i] + ad * dual_step(mu, d.shi[i], d.zhi[i], d.dshi[i]);
         wv -= zn;
         const double s = d.shi[i] + alpha * d.dshi[i];
         d.shi[i] = s;
@@ -1536,14 +1543,14 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
         // the slacks and multipliers D has just formed)
         const long i = wb + r;
         const RowBounds B(d, i, wb, (int)r);
-        const double slo = d.slo[B.lo], zlo = d.zlo[B.lo], dslo = d.dslo[B.lo], dzlo = d.dzlo[B.lo];
-        const double shi = d.shi[i], zhi = d.zhi[i], dshi = d.dshi[i], dzhi = d.dzhi[i];
+        const double slo = d.slo[B.lo], zlo = d.zlo[B.lo], dslo = d.dslo[B.lo];
+        const double shi = d.shi[i], zhi = d.zhi[i], dshi = d.dshi[i];
         double a[NF];
         const double v = row_va(d, 1 - S.cur, w, (int)r, S.xt, a);
         const double L = B.L(), U = B.U();
         double wv = 0, sl = slo, zl = zlo, sh = shi, zh = zhi;
         if (has_lo(d, L)) {
-            const double zn = zlo + ad * dzlo;
+            const double zn = zlo + ad * dual_step(mu, slo, zlo, dslo);
             wv += zn;
             sl = slo + alpha * dslo;
             zl = fmin(fmax(zn, mu / (ks * sl)), ks * mu / sl);
@@ -1551,7 +1558,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
             d.zlo[i] = zl;
         }
         if (has_hi(d, U)) {
-            const double zn = zhi + ad * dzhi;
+            const double zn = zhi + ad * dual_step(mu, shi, zhi, dshi);
             wv -= zn;
             sh = shi + alpha * dshi;
             zh = fmin(fmax(zn, mu / (ks * sh)), ks * mu / sh);
@@ -1772,8 +1779,8 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
         if (has_lo(d, L)) {
             const double s = slo, z = zlo, sg = z / s;
             const double ds = adx + rplo;
-            const double dz = mu / s - z - sg * ds;
-            d.dslo[i] = ds; d.dzlo[i] = dz;
+            const double dz = mu / s - z - sg * ds;  // = dual_step(mu, s, z, ds), formed again by pass D
+            d.dslo[i] = ds;
             if (ds < 0) ap = fmin(ap, -tau * s / ds);
             if (dz < 0) ad = fmin(ad, -tau * z / dz);
             rp1 += fabs(rplo); bdir += ds / s; logs += log(s);
@@ -1783,7 +1790,7 @@ __global__ __launch_bounds__(ROW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 
             const double s = shi, z = zhi, sg = z / s;
             const double ds = -adx + rphi;
             const double dz = mu / s - z - sg * ds;
-            d.dshi[i] = ds; d.dzhi[i] = dz;
+            d.dshi[i] = ds;
             if (ds < 0) ap = fmin(ap, -tau * s / ds);
             if (dz < 0) ad = fmin(ad, -tau * z / dz);
             rp1 += fabs(rphi); bdir += ds / s; logs += log(s);

@@ -429,7 +429,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     d.njn = (long)(jobs * NJ * Om * 3);
     d.njd = (long)(jobs * NJ * NF * 3);
     if ((rc = p->alloc(&d.jn, 2 * (size_t)d.njn)) || (rc = p->alloc(&d.jd, 2 * (size_t)d.njd))) return rc;
-    double** rowbufs[] = {&d.slo, &d.shi, &d.zlo, &d.zhi, &d.dslo, &d.dshi, &d.dzlo, &d.dzhi};
+    double** rowbufs[] = {&d.slo, &d.shi, &d.zlo, &d.zhi, &d.dslo, &d.dshi};
     for (double** b : rowbufs)
         if ((rc = p->alloc(b, Wm * Rmax))) return rc;
     const int nblk_max = (int)((Rmax + row_chunk() - 1) / row_chunk());
