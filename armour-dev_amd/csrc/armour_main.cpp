@@ -26,12 +26,23 @@
 // files, and the client exits with the server's status. Otherwise it plans in-process. The HIP
 // library is loaded with dlopen only on the in-process and server paths, so a served client never
 // maps the HIP runtime.
+// The request is one line: the client's buffer directory as an absolute path (realpath), the
+// horizon T and every ARMOUR_* setting of the client's environment that changes a plan (plan_env),
+// tab-separated. A server whose T or settings differ answers REFUSED and the client plans
+// in-process, so a server never plans another horizon or solver configuration than the client
+// would. The client truncates armour.out before it asks (MATLAB never reads a previous replan's
+// k_opt) and waits at most $ARMOUR_SERVE_TIMEOUT_MS (default 10000, the reference's time budget
+// scale) for the answer; a server that does not answer in time leaves -1 in armour.out and a
+// non-zero exit, as any failed replan.
 #include <dlfcn.h>
+#include <limits.h>
 #include <signal.h>
+#include <sys/time.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <charconv>
 #include <cstdio>
 #include <cstdlib>
@@ -42,6 +53,8 @@
 #include <vector>
 
 #include "../../include/armour_hip.h"
+
+extern char** environ;
 
 namespace {
 
@@ -250,21 +263,55 @@ bool fill_addr(sockaddr_un& a, const std::string& path) {
     return true;
 }
 
-// client: -1 when no server answers (plan in-process), else the server's exit status
+// ARMOUR_* settings of this process that change a plan (everything but the serving plumbing),
+// sorted, as "K=V" joined by ';': client and server must agree on them
+std::string plan_env() {
+    static const char* plumbing[] = {"ARMOUR_BUFFER_DIR=", "ARMOUR_SERVE_SOCKET=", "ARMOUR_NO_SERVE=",
+                                     "ARMOUR_SERVE_TIMEOUT_MS=", "ARMOUR_LIB="};
+    std::vector<std::string> kv;
+    for (char** e = environ; *e; e++) {
+        const std::string v = *e;
+        if (v.rfind("ARMOUR_", 0) != 0) continue;
+        bool skip = false;
+        for (const char* p : plumbing) skip = skip || v.rfind(p, 0) == 0;
+        if (!skip) kv.push_back(v);
+    }
+    std::sort(kv.begin(), kv.end());
+    std::string out;
+    for (const auto& v : kv) out += (out.empty() ? "" : ";") + v;
+    return out;
+}
+
+constexpr unsigned char SERVE_REFUSED = 254;  // server: T or settings differ (client plans in-process)
+
+// client: -1 when no server answers or the server refuses the request (plan in-process), else the
+// server's exit status
 int try_served(const std::string& dir) {
     sockaddr_un a;
     if (!fill_addr(a, socket_path(dir))) return -1;
+    char real[PATH_MAX];
+    if (!realpath(dir.c_str(), real)) return -1;  // in-process: it reports the missing directory
     const int fd = socket(AF_UNIX, SOCK_STREAM, 0);
     if (fd < 0) return -1;
     if (connect(fd, (sockaddr*)&a, sizeof(a)) != 0) {
         close(fd);
         return -1;
     }
-    const std::string req = dir + "\n";
+    const char* te = std::getenv("ARMOUR_SERVE_TIMEOUT_MS");
+    const long ms = te ? std::atol(te) : 10000;
+    timeval tv{ms / 1000, (ms % 1000) * 1000};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+    const std::string out1 = std::string(real) + "/armour.out";
+    { std::ofstream o(out1); }  // a fresh armour.out whatever the server does
+    const std::string req = std::string(real) + "\t" + std::to_string(time_steps()) + "\t" + plan_env() + "\n";
     unsigned char rc = 1;
-    const bool ok = write(fd, req.data(), req.size()) == (ssize_t)req.size() && read(fd, &rc, 1) == 1;
+    const bool sent = write(fd, req.data(), req.size()) == (ssize_t)req.size();
+    const bool got = sent && read(fd, &rc, 1) == 1;
     close(fd);
-    return ok ? (int)rc : 1;
+    if (got && rc == SERVE_REFUSED) return -1;
+    if (!got) return fail_out(out1, "the planning server did not answer (ARMOUR_SERVE_TIMEOUT_MS)");
+    return (int)rc;
 }
 
 std::string g_sock;
@@ -296,10 +343,13 @@ int serve(const Lib& L, const std::string& dir) {
     signal(SIGTERM, on_signal);
     signal(SIGINT, on_signal);
     signal(SIGPIPE, SIG_IGN);
+    const std::string env = plan_env();
     std::fprintf(stderr, "armour_main: serving %s (T = %d)\n", g_sock.c_str(), T);
     for (;;) {
         const int c = accept(fd, nullptr, nullptr);
         if (c < 0) continue;
+        timeval tv{5, 0};  // a client that connects and sends nothing does not hold the server
+        setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
         std::string req;
         char buf[512];
         ssize_t n;
@@ -307,9 +357,19 @@ int serve(const Lib& L, const std::string& dir) {
         const size_t e = req.find('\n');
         unsigned char rc = 1;
         if (e != std::string::npos) {
-            std::string d = req.substr(0, e);
-            if (!d.empty() && d.back() != '/') d += '/';
-            rc = (unsigned char)plan_dir(L, p, d);
+            // "<abs dir>\t<T>\t<settings>": plan only what this server's planner and environment
+            // would plan for the client (else REFUSED: the client plans in-process)
+            const std::string line = req.substr(0, e);
+            const size_t t1 = line.find('\t'), t2 = t1 == std::string::npos ? t1 : line.find('\t', t1 + 1);
+            if (t2 == std::string::npos || line.substr(t1 + 1, t2 - t1 - 1) != std::to_string(T) ||
+                line.substr(t2 + 1) != env) {
+                rc = SERVE_REFUSED;
+            } else {
+                std::string d = line.substr(0, t1);
+                if (!d.empty() && d.back() != '/') d += '/';
+                rc = (unsigned char)plan_dir(L, p, d);
+                if (rc == SERVE_REFUSED) rc = 1;
+            }
         }
         (void)!write(c, &rc, 1);
         close(c);

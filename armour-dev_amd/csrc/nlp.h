@@ -25,10 +25,18 @@ struct IpmOpts {
     double kappa_sigma = 1e10;
     double s_max = 100.0;
     double inf_bound = 1e19;
-    // barrier strategy: 0 monotone (default); 1 adaptive (ARMOUR_MU_STRATEGY=adaptive: the
-    // reference's IPOPT_MU_STRATEGY, KPR/Parameters.h:57, with the LOQO mu oracle and the kkt-error
-    // globalisation, as oracle/src/ipm.cpp; DESIGN.md §5 for why it is not the default)
-    int mu_strategy = 0;
+    // barrier strategy: 1 adaptive (default: the reference's IPOPT_MU_STRATEGY "adaptive",
+    // KPR/Parameters.h:57, restated with Ipopt's LOQO mu oracle and kkt-error globalisation, mu on a
+    // 2^(1/8) grid with floor tol / 10, as oracle/src/ipm.cpp); 0 monotone
+    // (ARMOUR_MU_STRATEGY=monotone)
+    int mu_strategy = 1;
+    // restoration phase (nlp_kernels.hip resto_*, oracle/src/ipm.cpp restoration): phases per
+    // solve (ARMOUR_RESTORATION=0: none), violation target inside the bounds, box barrier weight,
+    // stall ratio
+    int resto_max = 3;
+    double resto_delta = 1e-6;
+    double resto_mu = 1e-8;
+    double resto_stall = 1e-4;
 };
 
 struct WorldState {
@@ -41,7 +49,9 @@ struct WorldState {
     double filt_theta[MAX_FILTER], filt_phi[MAX_FILTER];
     int nfilt;
     int cur;           // eval slot holding the current point
-    int status;        // 0 running, 1 converged, 2 max_iter, 3 line-search failure, 4 reach over capacity
+    int status;        // 0 running, 1 converged, 2 max_iter, 3 line-search failure, 4 reach over capacity,
+                       // 5 local infeasibility (the restoration phase stalled or failed), 6 in the
+                       // restoration phase (WS_RESTO)
     int searching;     // 1 while the line search of this iteration has not accepted
     int accepted_ok;   // last acceptance passed the filter (0: forced after max_ls trials)
     int ftype;
@@ -51,7 +61,12 @@ struct WorldState {
     // (free mode: the last <= 4; fixed mode: the one at the switch)
     int free_mode, nref;
     double kkt_ref[4];
+    // restoration phase: phases entered, consecutive stalled iterations, a chosen step waiting
+    // for its full evaluation (applied by the next resto_world_G), Phi of the previous iteration
+    int nresto, rstall, rpend;
+    double rphi;
 };
+constexpr int WS_RESTO = 6;
 
 struct NlpDev {
     int W, T, NJ, O, m, R, nblk, chunk;
@@ -123,6 +138,9 @@ struct NlpDev {
     // ipm_world_Cs_all; the trial passes before it take the first step from pass B's partials
     // (pass_b_alpha) and every running world searches
     int b_in_cs;
+    // restoration launches: the trial and full evaluations take the worlds in the restoration
+    // phase (status WS_RESTO) instead of the searching ones
+    int resto;
     // Certified plane cache (plane_cache_kernel). The 36 planes of a buffered
     // obstacle and their offsets d, delta do not depend on x; only A . c(x) does. For every
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in

@@ -650,7 +650,8 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
     if ((mode == 1 || mode == 5) && d.lcount && blockIdx.y >= *d.lcount) return;
     const int t = blockIdx.x, w = world_of(d, blockIdx.y);
     WorldState& S = d.ws[w];
-    if (mode == 1 && !(S.status == 0 && S.searching)) return;
+    // (restoration launches, d.resto: the worlds in the restoration phase, WS_RESTO)
+    if (mode == 1 && !((d.resto ? S.status == WS_RESTO : S.status == 0) && S.searching)) return;
     if (mode == 5 && !(S.status == 0 && S.spec_k >= 0)) return;
     const int slot = mode == 0 ? 0 : 1 - S.cur;
     double* const Gb = d.g + gidx(d, slot, w, 0);
@@ -1360,10 +1361,14 @@ __global__ __launch_bounds__(64) void ipm_world_init(NlpDev d) {
     S.kkt = 0;
     S.free_mode = d.opt.mu_strategy == 1 ? 1 : 0;
     S.nref = 0;
+    S.nresto = 0;
+    S.rstall = 0;
+    S.rpend = 0;
+    S.rphi = -1;
 }
 
 __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_init(NlpDev d) {
-    const int w = blockIdx.y;
+    const int w = world_of(d, blockIdx.y);  // every world, or the list restarted by a restoration phase
     const WorldState& S = d.ws[w];
     const long r0 = (long)blockIdx.x * d.chunk;
     for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.R; r += blockDim.x) {
@@ -1644,6 +1649,27 @@ __device__ inline void world_partials_at(const double* base, int nblk, int strid
 }
 
 __device__ inline void world_A_body(const NlpDev& d, WorldState& S, int w, int nside);
+// The adaptive barrier parameter on a fixed logarithmic grid 2^(j/8) x 2^e (oracle/src/ipm.cpp
+// mu_grid, the same constants and comparisons): a rounding-level difference in the complementarity
+// sums leaves mu's bits unchanged unless it straddles a midpoint
+__device__ inline double mu_grid(double x) {
+    constexpr double G[9] = {0x1.0000000000000p+0, 0x1.172b83c7d517bp+0, 0x1.306fe0a31b715p+0,
+                             0x1.4bfdad5362a27p+0, 0x1.6a09e667f3bcdp+0, 0x1.8ace5422aa0dbp+0,
+                             0x1.ae89f995ad3adp+0, 0x1.d5818dcfba487p+0, 0x1.0000000000000p+1};
+    constexpr double B[8] = {0x1.0b5586cf9890fp+0, 0x1.2387a6e756238p+0, 0x1.3dea64c123422p+0,
+                             0x1.5ab07dd485429p+0, 0x1.7a11473eb0187p+0, 0x1.9c49182a3f090p+0,
+                             0x1.c199bdd85529cp+0, 0x1.ea4afa2a490dap+0};
+    if (!(x > 0) || !isfinite(x)) return x;
+    int e;
+    const double y = 2.0 * frexp(x, &e);
+    int j = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) j += y >= B[q];
+    double gj = G[0];
+#pragma unroll
+    for (int q = 1; q < 9; q++) gj = j == q ? G[q] : gj;
+    return ldexp(gj, e - 1);
+}
 // A world kernel (one wave) works on its world's state staged in LDS: one coalesced round trip in
 // and one out, where lane 0's steps would otherwise wait on a dependent global load per field
 __device__ inline void ws_copy(WorldState& dst, const WorldState& src) {
@@ -1685,7 +1711,9 @@ __device__ inline void world_A_body(const NlpDev& d, WorldState& S, int w, int n
     if (d.opt.mu_strategy == 1) {
         // adaptive barrier (oracle/src/ipm.cpp, same order of decisions): free mode takes mu from
         // the LOQO oracle; the kkt-error globalisation switches to fixed (monotone) mode when E0 has
-        // not fallen below 0.9999 x the largest of the last four, back once below the switch value
+        // not fallen below 0.9999 x the largest of the last four, back once below the switch value.
+        // mu on the 2^(1/8) grid, floor tol / 10
+        const double mu_min = d.opt.tol / 10;
         const double avg = P[53] / (double)(nside > 0 ? nside : 1), mn = P[54];
         bool progress = S.nref < 4;
         if (!progress) {
@@ -1696,7 +1724,7 @@ __device__ inline void world_A_body(const NlpDev& d, WorldState& S, int w, int n
         const double mu_old = S.mu;
         if (S.free_mode && !progress) {
             S.free_mode = 0;
-            S.mu = fmax(1e-11, 0.8 * avg);
+            S.mu = fmax(mu_min, mu_grid(0.8 * avg));
             S.kkt_ref[0] = E0;
             S.nref = 1;
         } else if (!S.free_mode && progress && S.nref >= 1 && E0 <= 0.9999 * S.kkt_ref[S.nref - 1]) {
@@ -1712,7 +1740,7 @@ __device__ inline void world_A_body(const NlpDev& d, WorldState& S, int w, int n
             }
             const double xi = mn / avg;
             const double sg = 0.1 * pow(fmin(0.05 * (1 - xi) / xi, 2.0), 3);
-            S.mu = fmax(1e-11, fmin(sg * avg, 1e5));
+            S.mu = fmax(mu_min, fmin(mu_grid(sg * avg), 1e5));
         } else if (Emu <= d.opt.kappa_eps * S.mu && S.mu > d.opt.tol / 10) {
             S.mu = fmax(d.opt.tol / 10, fmin(d.opt.kappa_mu * S.mu, pow(S.mu, d.opt.theta_mu)));
         }
@@ -1945,6 +1973,16 @@ __device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt,
     if (S.ls >= d.opt.max_ls) {  // keep the last trial (oracle: accepted = false)
         S.searching = 0;
         S.accepted_ok = 0;
+        if (S.nresto < d.opt.resto_max) {
+            // the restoration phase instead of the forced step (oracle/src/ipm.cpp 5b; run after the
+            // interior-point loop by planner.hip run_resto): the failed iteration counts
+            S.status = WS_RESTO;
+            S.nresto++;
+            S.iter++;
+            S.rphi = -1;
+            S.rstall = 0;
+            S.rpend = 0;
+        }
         return;
     }
     S.alpha *= 0.5;
@@ -2046,7 +2084,8 @@ __global__ __launch_bounds__(64) void ipm_world_Cs_all(NlpDev d) {
     if (valid) {
         ws_copy(S, d.ws[w]);
         __syncthreads();
-        if (d.b_in_cs) world_B_body(d, S, w);  // lane 0 writes what lane 0 alone reads below
+        if (d.b_in_cs) world_B_body(d, S, w);
+        __syncthreads();  // lane 0's WorldState stores before every lane's reads (filter_pass)
         world_Cs_body(d, S, blockIdx.x);
         __syncthreads();
         ws_copy(d.ws[w], S);
@@ -2196,6 +2235,261 @@ __global__ __launch_bounds__(64) void ipm_world_DA(NlpDev d, int nside) {
     world_A_body(d, S, w, nside);
     __syncthreads();
     ws_copy(d.ws[w], S);
+}
+
+// ------------------------------------------------------------------------------------------
+// Restoration phase (oracle/src/ipm.cpp restoration). A world whose line search
+// finds no acceptable trial (accept_trial) leaves the interior-point loop with status WS_RESTO;
+// planner.hip run_resto then takes all of them together, one iteration per round of launches:
+//   resto_rows_G / resto_world_G  the Gauss-Newton system of Phi at the current point, the
+//                                 decisions (every row within its bounds -> restart; the cap;
+//                                 stall) and the step with its largest fraction to the box;
+//   eval (mode 1) / resto_rows_V / resto_world_V  one Armijo trial per round, alpha halved, at
+//                                 most max_ls rounds (the oracle's sequential search).
+// The restarted worlds go back to the interior point (ipm_rows_init on their list, then the loop).
+constexpr int NRG = 37;  // pass G's partial sums: M (28, upper triangle), b (7), sum e^2, max original violation
+
+// the violation of one row against targets delta inside its bounds (e, and sg = -1 below the lower
+// target / +1 above the upper one) and against the bounds themselves (e0): ipm.cpp's expressions
+__device__ inline void resto_row(const NlpDev& d, double v, double L, double U, double& e, double& sg, double& e0) {
+    const double delta = d.opt.resto_delta;
+    e = 0; sg = 0; e0 = 0;
+    if (has_lo(d, L)) {
+        e0 = fmax(e0, L - v);
+        const double el = (L + delta) - v;
+        if (el > 0) { e = el; sg = -1.0; }
+    }
+    if (has_hi(d, U)) {
+        e0 = fmax(e0, v - U);
+        const double eh = v - (U - delta);
+        if (e == 0 && eh > 0) { e = eh; sg = 1.0; }
+    }
+}
+__device__ inline double resto_barrier(const NlpDev& d, const double* x) {
+    double b = 0;
+    for (int j = 0; j < NF; j++) b += -log(1.0 - x[j]) - log(1.0 + x[j]);
+    return d.opt.resto_mu * b;
+}
+
+__global__ __launch_bounds__(ROW_THREADS) void resto_rows_G(NlpDev d) {
+    const int w = world_of(d, blockIdx.y);
+    const WorldState& S = d.ws[w];
+    if (S.status != WS_RESTO) return;
+    __shared__ double lds[(ROW_THREADS / 64) * NRG];
+    const int slot = S.rpend ? 1 - S.cur : S.cur;  // a step chosen last iteration: its evaluation
+    double M[28], b[NF], V = 0, e0m = 0;
+#pragma unroll
+    for (int k = 0; k < 28; k++) M[k] = 0;
+#pragma unroll
+    for (int j = 0; j < NF; j++) b[j] = 0;
+    const long r0 = (long)blockIdx.x * d.chunk, wb = (long)w * d.R;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.m; r += blockDim.x) {
+        const long i = wb + r;
+        const RowBounds B(d, i, wb, (int)r);
+        double a[NF];
+        const double v = row_va(d, slot, w, (int)r, S.x, a);
+        double e, sg, e0;
+        resto_row(d, v, B.L(), B.U(), e, sg, e0);
+        e0m = fmax(e0m, e0);
+        if (e > 0) {
+            V += e * e;
+            const double es = e * sg;
+            int k = 0;
+#pragma unroll
+            for (int p = 0; p < NF; p++) {
+                b[p] += es * a[p];
+#pragma unroll
+                for (int q = p; q < NF; q++) M[k++] += a[p] * a[q];
+            }
+        }
+    }
+    double v[NRG];
+    int kinds[NRG];
+#pragma unroll
+    for (int k = 0; k < 28; k++) v[k] = M[k];
+#pragma unroll
+    for (int j = 0; j < NF; j++) v[28 + j] = b[j];
+    v[35] = V;
+    v[36] = e0m;
+#pragma unroll
+    for (int k = 0; k < NRG; k++) kinds[k] = k == 36 ? 1 : 0;
+    block_reduce_n(v, kinds, lds, d.partial + ((long)w * d.nblk + blockIdx.x) * KA);
+}
+
+// a restoration phase that reached a point within every bound hands the world back to the
+// interior point: a fresh filter and BFGS matrix at the current mu (slacks: ipm_rows_init)
+__device__ inline void resto_restart(const NlpDev& d, WorldState& S) {
+    S.status = 0;
+    for (int i = 0; i < NF * NF; i++) S.H[i] = (i % (NF + 1) == 0) ? 1.0 : 0.0;
+    S.first_update = 1;
+    S.nfilt = 0;
+    S.theta_max = -1;
+    S.theta_min = -1;
+    S.nfail = 0;
+    S.free_mode = d.opt.mu_strategy == 1 ? 1 : 0;
+    S.nref = 0;
+    S.searching = 0;
+    S.spec_k = -1;
+}
+
+// pass G's world step (lane 0 after the partials): ipm.cpp restoration's order of decisions
+__device__ inline void resto_step(const NlpDev& d, WorldState& S, const double (&P)[NRG]) {
+    if (P[36] <= 0) { resto_restart(d, S); return; }
+    if (S.iter >= d.opt.max_iter) { S.status = 2; return; }
+    const double V = P[35];
+    const double phi = 0.5 * V + resto_barrier(d, S.x);
+    if (S.rphi >= 0) {
+        S.rstall = (S.rphi - phi <= d.opt.resto_stall * S.rphi) ? S.rstall + 1 : 0;
+        if (S.rstall >= 2) { S.status = 5; return; }
+    }
+    S.rphi = phi;
+    double A[NF * NF], rhs[NF], gp[NF], dx[NF];
+    int k = 0;
+    for (int p = 0; p < NF; p++)
+        for (int q = p; q < NF; q++) {
+            A[p * NF + q] = P[k];
+            A[q * NF + p] = P[k];
+            k++;
+        }
+    double dmax = 0;
+    for (int j = 0; j < NF; j++) dmax = fmax(dmax, A[j * NF + j]);
+    const double lam = 1e-2 * fmin(1.0, sqrt(V)) * (1.0 + dmax);
+    const double mr = d.opt.resto_mu;
+    for (int j = 0; j < NF; j++) {
+        const double u = 1.0 - S.x[j], l = 1.0 + S.x[j];
+        gp[j] = P[28 + j] + mr * (1.0 / u - 1.0 / l);
+        A[j * NF + j] += mr * (1.0 / (u * u) + 1.0 / (l * l)) + lam;
+        rhs[j] = -gp[j];
+    }
+    double shift = 0.0;
+    bool ok = false;
+    for (int tries = 0; tries < 40 && !ok; tries++) {
+        ok = chol_solve7(A, shift, rhs, dx);
+        shift = (shift == 0.0) ? 1e-8 : shift * 10;
+    }
+    if (!ok) { S.status = 5; return; }
+    double amax = 1.0, dphi = 0;
+    for (int j = 0; j < NF; j++) {
+        if (dx[j] > 0) amax = fmin(amax, d.opt.tau_min * (1.0 - S.x[j]) / dx[j]);
+        if (dx[j] < 0) amax = fmin(amax, d.opt.tau_min * (-1.0 - S.x[j]) / dx[j]);
+        dphi += gp[j] * dx[j];
+    }
+    for (int j = 0; j < NF; j++) {
+        S.dx[j] = dx[j];
+        S.xt[j] = S.x[j] + amax * dx[j];
+    }
+    S.alpha = amax;
+    S.phi0 = phi;
+    S.Dphi = dphi;
+    S.searching = 1;
+    S.ls = 0;
+}
+
+// the last block of a restoration launch publishes a count (worlds still in the phase / still
+// searching) into the mapped host flags and resets the ticket counters
+__device__ inline void resto_count(const NlpDev& d, bool mine, int flag) {
+    if (mine) atomicAdd(&d.cnt[0], 1u);
+    __threadfence();
+    if (atomicAdd(&d.cnt[2], 1u) == gridDim.x - 1) {
+        __threadfence();
+        d.flags[flag] = (int)atomicAdd(&d.cnt[0], 0u);
+        d.cnt[0] = 0;
+        d.cnt[2] = 0;
+    }
+}
+
+__global__ __launch_bounds__(64) void resto_world_G(NlpDev d) {
+    const int w = world_of(d, blockIdx.x);
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    if (S.status == WS_RESTO) {
+        double P[NRG], init[NRG];
+        int op[NRG];
+#pragma unroll
+        for (int k = 0; k < NRG; k++) { init[k] = 0; op[k] = k == 36 ? 1 : 0; }
+        world_partials(d, w, init, op, P);
+        if (threadIdx.x == 0) {
+            if (S.rpend) {  // the step chosen last iteration, evaluated in the trial slot
+                for (int j = 0; j < NF; j++) S.x[j] = S.xt[j];
+                S.cur = 1 - S.cur;
+                S.iter++;
+                S.rpend = 0;
+            }
+            resto_step(d, S, P);
+        }
+    }
+    __syncthreads();
+    ws_copy(d.ws[w], S);
+    if (threadIdx.x == 0) resto_count(d, S.status == WS_RESTO, 0);
+}
+
+// sum e^2 at the trial point (the trial slot's full evaluation, mode 1)
+__global__ __launch_bounds__(ROW_THREADS) void resto_rows_V(NlpDev d) {
+    const int w = world_of(d, blockIdx.y);
+    const WorldState& S = d.ws[w];
+    if (!(S.status == WS_RESTO && S.searching)) return;
+    __shared__ double lds[(ROW_THREADS / 64) * NRG];
+    const int slot = 1 - S.cur;
+    double V = 0;
+    const long r0 = (long)blockIdx.x * d.chunk, wb = (long)w * d.R;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.m; r += blockDim.x) {
+        const long i = wb + r;
+        const RowBounds B(d, i, wb, (int)r);
+        const double v = d.g[gidx(d, slot, w, r)];
+        double e, sg, e0;
+        resto_row(d, v, B.L(), B.U(), e, sg, e0);
+        V += e * e;
+    }
+    double vv[1] = {V};
+    const int kinds[1] = {0};
+    block_reduce_n(vv, kinds, lds, d.partial + ((long)w * d.nblk + blockIdx.x) * KA);
+}
+
+// the Armijo test of the round's trial; a rejected trial halves alpha (max_ls trials, then the
+// phase fails: local infeasibility at the current point)
+__global__ __launch_bounds__(64) void resto_world_V(NlpDev d) {
+    const int w = world_of(d, blockIdx.x);
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    if (S.status == WS_RESTO && S.searching) {
+        double P[1];
+        const double init[1] = {0.0};
+        const int op[1] = {0};
+        world_partials(d, w, init, op, P);
+        if (threadIdx.x == 0) {
+            S.nevals++;
+            const double phit = 0.5 * P[0] + resto_barrier(d, S.xt);
+            if (phit <= S.phi0 + d.opt.eta * S.alpha * S.Dphi) {
+                S.searching = 0;
+                S.rpend = 1;
+            } else if (++S.ls >= d.opt.max_ls) {
+                S.searching = 0;
+                S.status = 5;
+            } else {
+                S.alpha *= 0.5;
+                for (int j = 0; j < NF; j++) S.xt[j] = S.x[j] + S.alpha * S.dx[j];
+            }
+        }
+    }
+    __syncthreads();
+    ws_copy(d.ws[w], S);
+    if (threadIdx.x == 0) resto_count(d, S.status == WS_RESTO && S.searching, 1);
+}
+
+// the worlds of list `in` (n entries; null: worlds 0..n-1) with status `st`, into `out`; the count
+// into the mapped host flag `flag` (one block)
+__global__ __launch_bounds__(1024) void ipm_collect(NlpDev d, const int* in, int n, int st, int* out, int flag) {
+    __shared__ unsigned c;
+    if (threadIdx.x == 0) c = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int w = in ? in[i] : i;
+        if (d.ws[w].status == st) out[atomicAdd(&c, 1u)] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) d.flags[flag] = (int)c;
 }
 
 // finalize_solution's feasibility re-check (NLPclass.cu:449-538): one block per world

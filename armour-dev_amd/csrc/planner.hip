@@ -72,6 +72,7 @@ struct armour_planner {
     unsigned* d_done = nullptr;            // workgroups finished in the current reach launch
     long long* h_sum = nullptr;            // mapped host: reach counters published by the last workgroup
     ReachCounters rc{};                    // (reach_kernel.hip)
+    long long reach_seq = 0;               // sequence number of the last reach launch (ReachCounters::seq)
     int* d_wlist = nullptr;                // [max_worlds] worlds of a capacity retry
     int last_retried = 0, last_failed = 0;
     std::vector<int> world_err;            // per world of the last batch: 0 or ARMOUR_E_CAPACITY
@@ -100,6 +101,7 @@ struct armour_planner {
     int last_shape = 0;       // shape of the last first launch (a capacity retry uses it too)
     int dev = 0;              // the planner's device
     bool counted = false;     // counted in g_planners[dev]
+    bool device_shared = false;  // ARMOUR_DEVICE_SHARED=1: other processes plan on this GPU too
     lane::LaneArgs la;
 
     // nlp
@@ -157,6 +159,10 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     p->dev = dev;
     g_planners[dev & 63]++;
     p->counted = true;
+    // g_planners sees this process's planners only; planners of other processes on the same GPU
+    // (torchrun ranks folded onto one device, several armour_main servers) are declared with
+    // ARMOUR_DEVICE_SHARED=1 (it only chooses the bundle kernel's shape)
+    if (const char* e = std::getenv("ARMOUR_DEVICE_SHARED")) p->device_shared = std::atoi(e) != 0;
     HIPCK(hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (robot) {
         if (!robot_from_tables(*robot, p->rp))
@@ -311,7 +317,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         long long* dsum = nullptr;
         HIPCK(hipHostMalloc((void**)&p->h_sum, sizeof(long long) * (RSUM_ERR + (size_t)Wm), hipHostMallocMapped));
         HIPCK(hipHostGetDevicePointer((void**)&dsum, p->h_sum, 0));
-        p->rc = ReachCounters{p->d_bytes, p->d_occ, p->d_done, dsum};
+        p->rc = ReachCounters{p->d_bytes, p->d_occ, p->d_done, dsum, 0};
+        p->h_sum[RSUM_SEQ] = 0;
         ra.rc = p->rc;
         ra.ntq = p->armtd ? 0 : NF;
     }
@@ -408,8 +415,11 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     d.NJ = NJ;
     d.ro = ro;
     if (cfg->max_iter > 0) d.opt.max_iter = cfg->max_iter;
-    if (const char* ms = std::getenv("ARMOUR_MU_STRATEGY"))  // the reference's adaptive barrier (option)
-        d.opt.mu_strategy = std::strcmp(ms, "adaptive") == 0 ? 1 : 0;
+    if (const char* ms = std::getenv("ARMOUR_MU_STRATEGY"))  // adaptive (default) or monotone
+        d.opt.mu_strategy = std::strcmp(ms, "monotone") == 0 ? 0 : 1;
+    if (const char* rs = std::getenv("ARMOUR_RESTORATION"))  // restoration phases per solve (0: none)
+        d.opt.resto_max = std::atoi(rs) < 0 ? 0 : std::atoi(rs);
+    d.resto = 0;
     d.armtd = p->armtd ? 1 : 0;
     d.nt = p->armtd ? 0 : NF * T;
     d.krange = nullptr;
@@ -550,13 +560,15 @@ static int upload_armtd(armour_planner* p, int W, const armour_armtd_world* worl
 
 // Bundle kernel shape of a launch of `bundles` bundles (lane_kernel.hip): the dense shape (three
 // per CU) when the batch does not fit one round of the wide shape (two per CU), or when other
-// planners share the device and the batch holds more than one bundle per CU; else the wide shape.
+// planners share the device (this process's live planners, or ARMOUR_DEVICE_SHARED=1 for planners
+// in other processes) and the batch holds more than one bundle per CU; else the wide shape.
 // Measured: three planners x 327 worlds dense 5324-5363 against 5187 plans/s;
 // three planners x 85 worlds (config 4's 256-world job) wide 63.5 against 72.1 ms.
 static int lane_shape_for(armour_planner* p, long bundles) {
     int shape = p->lane_shape;
     if (shape < 0)
-        shape = (bundles > p->lane_slots[0] || (g_planners[p->dev & 63].load() > 1 && bundles > p->reach_cus)) ? 1 : 0;
+        shape = (bundles > p->lane_slots[0] ||
+                 ((p->device_shared || g_planners[p->dev & 63].load() > 1) && bundles > p->reach_cus)) ? 1 : 0;
     p->last_shape = shape;
     return shape;
 }
@@ -594,11 +606,13 @@ static int run_reach(armour_planner* p) {
         hipLaunchKernelGGL(jrs_kernel, dim3((int)((nj + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
                            p->qdd0, p->d_jrs, p->rc, p->ro.err);
     ra.jrs = p->d_jrs;
+    ra.rc.seq = ++p->reach_seq;
     if (p->lane_engine) {
         lane::LaneArgs la = p->la;
         la.W = p->W;
         la.T = p->T;
         la.jrs = p->d_jrs;
+        la.rc.seq = p->reach_seq;
         const long bundles = (jobs + lane::LG - 1) / lane::LG;
         const int shape = lane_shape_for(p, bundles);
         const long slots = std::min<long>(p->lane_slots[shape], p->lane_grid);
@@ -615,6 +629,8 @@ static int run_reach(armour_planner* p) {
     HIPCK(hipEventRecord(p->ev[4], rs));
     HIPCK(hipEventSynchronize(p->ev[4]));
     const volatile long long* sum = p->h_sum;
+    if (sum[RSUM_SEQ] != p->reach_seq)
+        return fail(ARMOUR_E_HIP, "reach kernel finished without publishing its counters (sequence number mismatch)");
     std::vector<int> err(p->W);
     for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
     for (int k = 0; k < 8; k++) p->h_occ[k] = (unsigned long long)sum[1 + k];
@@ -648,6 +664,7 @@ static int run_reach(armour_planner* p) {
         la.nlist = (int)retry.size();
         la.dump = nullptr;   // the op dump and bundle times stay those of the first launch
         la.btime = nullptr;
+        la.rc.seq = ++p->reach_seq;
         HIPCK(hipMemcpyAsync(p->d_wlist, retry.data(), sizeof(int) * retry.size(), hipMemcpyHostToDevice, rs));
         HIPCK(hipMemsetAsync(p->ro.err, 0, sizeof(int) * p->W, rs));
         const long bundles = ((long)retry.size() * p->T + lane::LG - 1) / lane::LG;
@@ -656,6 +673,8 @@ static int run_reach(armour_planner* p) {
         HIPCK(hipGetLastError());
         HIPCK(hipEventRecord(p->ev[5], rs));
         HIPCK(hipEventSynchronize(p->ev[5]));
+        if (sum[RSUM_SEQ] != p->reach_seq)
+            return fail(ARMOUR_E_HIP, "capacity retry finished without publishing its counters (sequence number mismatch)");
         for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
         mono[0] = (unsigned long long)sum[1 + 3];   // maxima over both launches (occ accumulates)
         mono[1] = (unsigned long long)sum[1 + 4];
@@ -714,19 +733,13 @@ static void launch_eval(armour_planner* p, dim3 grid, const NlpDev& d, int mode,
     hipLaunchKernelGGL(k, grid, dim3(EVAL_THREADS), 0, p->stream, d, mode);
 }
 
-static int run_solver(armour_planner* p) {
+// The interior-point loop over the nrun worlds listed in the first iteration list (d_lists[0..]):
+// every world there starts an iteration with pass A at its current point (a fresh solve, or a
+// restart after a restoration phase).
+static int ipm_loop(armour_planner* p, int nrun) {
     NlpDev& d = p->d;
-    const int W = p->W;
     int* Li[2] = {p->d_lists, p->d_lists + p->Wmax};                  // worlds of an iteration
     int* Ls[2] = {p->d_lists + 2 * p->Wmax, p->d_lists + 3 * p->Wmax};  // worlds of a line-search round
-    d.wl = nullptr;
-    d.wl_run = Li[0];
-    d.ls0 = 0;
-    ensure_plane_cache(p);
-    hipLaunchKernelGGL(ipm_world_init, dim3((W + 63) / 64), dim3(64), 0, p->stream, d);
-    launch_eval(p, dim3(p->T, W), d, 0);
-    hipLaunchKernelGGL(ipm_rows_init, dim3(d.nblk, W), dim3(ROW_THREADS), 0, p->stream, d);
-    HIPCK(hipGetLastError());
     const int ns = nside_count(p);
     // Launches cover the active worlds only (NlpDev::wl): every line-search round's ipm_world_C
     // compacts the worlds still running / still searching into the next lists and publishes the
@@ -740,14 +753,14 @@ static int run_solver(armour_planner* p) {
     // searching count in cnt[5]), and the host learns iteration it's running count one iteration
     // later (event tev[it & 1], flags[2 + (it & 1)]). Blocks past a list's length exit at once, so a
     // world's arithmetic is that of the synchronised loop.
-    int cur = 0, nrun = W;
+    int cur = 0;
     bool tail = false;       // iteration it - 1 ran sync-free (its running count not yet read)
     // worlds that backtracked (searched past round 0) in the latest iteration the host knows of: the
     // tail takes the one-round search while they do (ARMOUR_TAIL_SEARCH=adaptive). A converging
     // world mostly accepts round 0's trial, which its own full evaluation serves faster than the
     // values of every trial plus the chosen one's full evaluation; a backtracking world saves a
     // round. The choice changes launches only, never a world's arithmetic.
-    int backtracked = W;
+    int backtracked = nrun;
     for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
         const bool tl = it > 0 && p->spec && d.pcready && nrun <= p->tail_worlds;
         NlpDev di = d;
@@ -878,11 +891,81 @@ static int run_solver(armour_planner* p) {
                 hipLaunchKernelGGL(ipm_world_C, dim3(nsearch), dim3(64), 0, p->stream, dc);
             }
         }
-        if (nnext == 0) break;  // every world converged, hit the cap or failed
+        if (nnext == 0) break;  // every world converged, hit the cap, failed or left for restoration
         HIPCK(hipGetLastError());
         cur = 1 - cur;
         nrun = nnext;
     }
+    HIPCK(hipGetLastError());
+    return 0;
+}
+
+// One restoration phase for the n worlds of `list` (status WS_RESTO), all together: per iteration
+// the Gauss-Newton pass and world step, then the Armijo search one trial per round (a full
+// evaluation into the trial slot each; rounds after the first are launched without a host
+// synchronisation, their blocks exit for worlds that stopped searching). The worlds leave with
+// status 0 (every row within its bounds: restart), 2 (iteration cap) or 5 (local infeasibility).
+static int run_resto(armour_planner* p, const int* list, int n) {
+    NlpDev dr = p->d;
+    dr.wl = list;
+    dr.resto = 1;
+    dr.lcount = nullptr;
+    const volatile int* fl = p->h_flags;
+    for (int guard = 0; guard < 4 * (dr.opt.max_iter + 1); guard++) {
+        hipLaunchKernelGGL(resto_rows_G, dim3(dr.nblk, n), dim3(ROW_THREADS), 0, p->stream, dr);
+        hipLaunchKernelGGL(resto_world_G, dim3(n), dim3(64), 0, p->stream, dr);
+        HIPCK(hipStreamSynchronize(p->stream));
+        if (fl[0] == 0) break;
+        for (int ls = 0; ls < dr.opt.max_ls; ls++) {
+            launch_eval(p, dim3(p->T, n), dr, 1);
+            hipLaunchKernelGGL(resto_rows_V, dim3(dr.nblk, n), dim3(ROW_THREADS), 0, p->stream, dr);
+            hipLaunchKernelGGL(resto_world_V, dim3(n), dim3(64), 0, p->stream, dr);
+            if (ls == 0) {
+                HIPCK(hipStreamSynchronize(p->stream));
+                if (fl[1] == 0) break;
+            }
+        }
+        HIPCK(hipGetLastError());
+    }
+    return 0;
+}
+
+static int run_solver(armour_planner* p) {
+    NlpDev& d = p->d;
+    const int W = p->W;
+    int* Li0 = p->d_lists;                  // the interior-point loop's first list
+    int* Lr = p->d_lists + 2 * p->Wmax;     // worlds of a restoration phase
+    d.wl = nullptr;
+    d.wl_run = Li0;
+    d.ls0 = 0;
+    d.resto = 0;
+    ensure_plane_cache(p);
+    hipLaunchKernelGGL(ipm_world_init, dim3((W + 63) / 64), dim3(64), 0, p->stream, d);
+    launch_eval(p, dim3(p->T, W), d, 0);
+    hipLaunchKernelGGL(ipm_rows_init, dim3(d.nblk, W), dim3(ROW_THREADS), 0, p->stream, d);
+    HIPCK(hipGetLastError());
+    int rc = ipm_loop(p, W);
+    // Restoration phases: the worlds whose line search failed left the loop with
+    // status WS_RESTO. They run their phase together; those that reached a point within every bound
+    // restart the interior point (slacks and multipliers at that point), and may fail again (at
+    // most resto_max phases per world, S.nresto).
+    const volatile int* fl = p->h_flags;
+    while (rc == 0 && d.opt.resto_max > 0) {
+        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, WS_RESTO, Lr, 0);
+        HIPCK(hipStreamSynchronize(p->stream));
+        const int nr = fl[0];
+        if (nr == 0) break;
+        if ((rc = run_resto(p, Lr, nr))) break;
+        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)Lr, nr, 0, Li0, 0);
+        HIPCK(hipStreamSynchronize(p->stream));
+        const int ni = fl[0];
+        if (ni == 0) break;
+        NlpDev di = d;
+        di.wl = Li0;
+        hipLaunchKernelGGL(ipm_rows_init, dim3(d.nblk, ni), dim3(ROW_THREADS), 0, p->stream, di);
+        rc = ipm_loop(p, ni);
+    }
+    if (rc) return rc;
     // feasibility re-check and the sliced link centres at the final iterate (the current slot's,
     // armour_joint_position_center.out payload)
     hipLaunchKernelGGL(feasible_kernel, dim3(W), dim3(256), 0, p->stream, d, p->feas);
@@ -1128,7 +1211,7 @@ static int plan_uploaded(armour_planner* p, armour_result* results, armour_timin
         armour_result& r = results[w];
         for (int i = 0; i < NF; i++) r.k_opt[i] = S.x[i];
         r.feasible = p->h_feas[w];
-        r.solver_status = S.status == 1 ? 0 : S.status == 2 ? 1 : S.status == 3 ? 2 : 3;
+        r.solver_status = S.status == 1 ? 0 : S.status == 2 ? 1 : S.status == 3 ? 2 : S.status == 5 ? 4 : 3;
         r.iterations = S.iter;
         r.evaluations = S.nevals;
         r.cost = p->h_f[S.cur * p->d.W + w] / p->rp.cost_scale;

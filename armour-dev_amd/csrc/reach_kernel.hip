@@ -31,15 +31,20 @@ constexpr int POOL_DOUBLES = 1024;   // handle payloads (ProgramBuilder::slot_of
 // The reach phase's counters: the algorithmic byte count, the capacity maxima occ[8] (arena
 // hashes, arena rows, operator terms, link / torque k-only monomials) and the per-world error
 // flags. jrs_kernel zeroes them; the reach kernel's last workgroup publishes them in mapped host
-// memory (hsum[0] bytes, hsum[1..8] occ, hsum[RSUM_ERR + w] world w's flags). So the host reads
-// them after one event wait, and no fill or copy runs on the reach stream: under concurrent
-// planners such a blit kernel would wait for CUs another planner's persistent reach kernel holds.
-constexpr int RSUM_ERR = 9;
+// memory (hsum[0] bytes, hsum[1..8] occ, hsum[RSUM_ERR + w] world w's flags, and last
+// hsum[RSUM_SEQ] = the launch's sequence number). So the host reads them after one event wait, and
+// no fill or copy runs on the reach stream: under concurrent planners such a blit kernel would wait
+// for CUs another planner's persistent reach kernel holds. The host checks the sequence number
+// before it trusts the other words (a launch whose last workgroup did not publish fails loudly
+// instead of leaving the previous batch's flags and capacities in place).
+constexpr int RSUM_SEQ = 9;
+constexpr int RSUM_ERR = 10;
 struct ReachCounters {
     unsigned long long* bytes;  // [1]
     unsigned long long* occ;    // [8]
     unsigned* done;             // [1] workgroups finished (the last one resets it to 0)
     long long* hsum;            // mapped host [RSUM_ERR + W]
+    long long seq;              // this launch's sequence number (planner.hip run_reach)
 };
 
 __device__ inline void zero_counters(const ReachCounters& c, int* err, int W) {
@@ -65,6 +70,11 @@ __device__ inline void publish_counters(const ReachCounters& c, int* err, int W,
     if (threadIdx.x == 0) {
         c.hsum[0] = (long long)atomicAdd(c.bytes, 0ull);
         atomicExch(c.done, 0u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        c.hsum[RSUM_SEQ] = c.seq;  // after every other word of this launch
     }
 }
 

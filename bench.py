@@ -69,6 +69,9 @@ def parse():
                          "Fetch arm from its URDF (config 5, at fp64)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="per CPU-baseline leg (0: skip)")
     ap.add_argument("--no-extras", action="store_true", help="skip the N=1 extras (latency, copy peak, roofline)")
+    ap.add_argument("--dump-records", default="",
+                    help="rank 0 saves the last step's gathered per-world records (armour_amd.dist.RECORD layout, "
+                         "world order) to this .npy file (tests/test_gpu_dist.py compares them with the oracle)")
     return ap.parse_args()
 
 
@@ -334,6 +337,8 @@ def main():
     if rank != 0:
         dist.destroy_process_group()
         return
+    if a.dump_records:
+        np.save(a.dump_records, allrec)
     total_plans = a.steps * total_job
     value = total_plans / elapsed
     n_feas = int(allrec[:, 8].sum())
@@ -369,7 +374,8 @@ def main():
                    "mean_evaluations": float(np.mean([r["evaluations"] for r in res])),
                    "iteration_limit": 100,
                    "status_counts": {k: int(sum(r["status"] == c for r in res))
-                                     for k, c in (("converged", 0), ("iteration_limit", 1), ("line_search_failure", 2))}},
+                                     for k, c in (("converged", 0), ("iteration_limit", 1), ("line_search_failure", 2),
+                                                  ("local_infeasibility", 4))}},
         "roofline": None,
         "cpu_baseline": None,
     }

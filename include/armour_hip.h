@@ -56,7 +56,10 @@ typedef struct armour_world {
 typedef struct armour_result {
     double k_opt[ARMOUR_NUM_FACTORS]; /* normalised, in [-1, 1] (MATLAB scales by pi/48) */
     int feasible;        /* finalize_solution re-check (KPR/NLPclass.cu:449-538) */
-    int solver_status;   /* 0 converged, 1 iteration cap, 2 line-search failure, 3 not planned (see error) */
+    int solver_status;   /* 0 converged, 1 iteration cap, 2 line-search failure (no restoration phase
+                            left), 3 not planned (see error), 4 local infeasibility (the restoration
+                            phase found no point within the bounds: Ipopt's Infeasible_Problem_Detected
+                            role) */
     int iterations;
     int evaluations;
     double cost;         /* objective / COST_FUNCTION_OPTIMALITY_SCALE at k_opt */

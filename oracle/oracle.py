@@ -50,6 +50,8 @@ def lib():
                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.oracle_plan.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, ctypes.c_int]
         L.oracle_plan_mu.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, ctypes.c_int, ctypes.c_int]
+        L.oracle_plan_ex.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_double]
         _LIB = L
     return _LIB
 
@@ -155,13 +157,13 @@ class OraclePlanner:
         return dict(rows=r.value, cols=cl.value, center=c[:k], indep=ind[:k], hashes=hs[:n],
                     coeffs=co[:n, :k])
 
-    def plan(self, max_iter=0, mu_strategy=0):
-        """mu_strategy 0: monotone barrier (the build's solver); 1: adaptive (KPR/Parameters.h:57's
-        strategy, an option: DESIGN.md §5)"""
+    def plan(self, max_iter=0, mu_strategy=1, flags=0, noise=0.0):
+        """mu_strategy 1: adaptive barrier (the default, KPR/Parameters.h:57's strategy); 0: monotone
+        (an option: DESIGN.md §5). flags / noise: oracle_plan_ex (capi.cpp), studies only"""
         k = np.zeros(7)
         g = np.zeros(self.m)
         stats = np.zeros(8)
-        feas = lib().oracle_plan_mu(self.h, _ptr(k), _ptr(g), _ptr(stats), max_iter, mu_strategy)
+        feas = lib().oracle_plan_ex(self.h, _ptr(k), _ptr(g), _ptr(stats), max_iter, mu_strategy, flags, noise)
         if feas < 0:
             raise RuntimeError("oracle plan failed")
         return dict(k_opt=k, feasible=bool(feas), g=g, reach_ms=stats[0], nlp_ms=stats[1],

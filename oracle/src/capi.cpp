@@ -24,7 +24,20 @@ struct PlannerNlp : IpmProblem {
         *f = P->eval_f(x);
         P->eval_grad_f(x, grad);
         P->eval_g_jac(x, g, jac);
+        if (noise > 0) {
+            // sensitivity study only: g and J scaled by 1 + noise u, u uniform in [-1, 1), a fixed
+            // xorshift sequence per solve (tools/mu_study.py --noise)
+            const int m = P->m();
+            for (long i = 0; i < (long)m * (NF + 1); i++) {
+                rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17;
+                const double u = (double)(rng >> 11) * 0x1p-52 - 1.0;
+                if (i < m) g[i] *= 1.0 + noise * u;
+                else if (jac) jac[i - m] *= 1.0 + noise * u;
+            }
+        }
     }
+    double noise = 0;
+    unsigned long long rng = 0x9E3779B97F4A7C15ull;
 };
 
 Robot robot_by_id(int id) {
@@ -232,11 +245,20 @@ int oracle_pz(void* h, int kind, int idx, double* center, double* indep, unsigne
 // [4]=solver status, [5]=objective/cost_scale, [6]=kkt error. Returns 1 feasible, 0 infeasible, -1 error.
 int oracle_plan_mu(void* h, double* k_opt, double* g_out, double* stats, int max_iter, int mu_strategy);
 int oracle_plan(void* h, double* k_opt, double* g_out, double* stats, int max_iter) {
-    return oracle_plan_mu(h, k_opt, g_out, stats, max_iter, 0);
+    return oracle_plan_mu(h, k_opt, g_out, stats, max_iter, 1);
 }
 
-// the same with the barrier strategy chosen (0 monotone, the default; 1 adaptive: DESIGN.md §5)
+// the same with the barrier strategy chosen (1 adaptive, the default: IPOPT_MU_STRATEGY "adaptive",
+// KPR/Parameters.h:57; 0 monotone: DESIGN.md §5)
+int oracle_plan_ex(void* h, double* k_opt, double* g_out, double* stats, int max_iter, int mu_strategy, int flags,
+                   double noise);
 int oracle_plan_mu(void* h, double* k_opt, double* g_out, double* stats, int max_iter, int mu_strategy) {
+    return oracle_plan_ex(h, k_opt, g_out, stats, max_iter, mu_strategy, 0, 0.0);
+}
+// flags: bits 0-1 IpmOptions::mu_study, bit 2 no restoration phase; noise: relative perturbation of
+// every g / J value the solver sees (sensitivity studies only)
+int oracle_plan_ex(void* h, double* k_opt, double* g_out, double* stats, int max_iter, int mu_strategy, int flags,
+                   double noise) {
     Planner* P = static_cast<Planner*>(h);
     auto t0 = std::chrono::high_resolution_clock::now();
     try {
@@ -246,10 +268,13 @@ int oracle_plan_mu(void* h, double* k_opt, double* g_out, double* stats, int max
     }
     auto t1 = std::chrono::high_resolution_clock::now();
     PlannerNlp nlp(P);
+    nlp.noise = noise;
     IpmOptions opt;
     opt.tol = P->tol;
     if (max_iter > 0) opt.max_iter = max_iter;
     opt.mu_strategy = mu_strategy;
+    opt.mu_study = flags & 3;
+    if (flags & 4) opt.resto_max = 0;  // no restoration phase (studies)
     double x[NF] = {0, 0, 0, 0, 0, 0, 0};  // NLPclass.cu:193-199
     std::vector<double> g(P->m());
     IpmResult r = ipm_solve(nlp, opt, x, g.data());

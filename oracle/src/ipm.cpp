@@ -14,6 +14,27 @@ namespace oracle {
 
 static const int NMAX = 8;
 
+// The barrier parameter on a fixed logarithmic grid, 2^(j/8) x 2^e: the nearest grid point in
+// log2 (ties up), with the grid values and the midpoints between them as exact constants so that
+// the device solver (nlp_kernels.hip mu_grid) forms the same bits. The adaptive rule's mu is a
+// smooth function of the complementarity products; on the grid a rounding-level difference in
+// those sums leaves mu unchanged (unless it straddles a midpoint), where the LOQO sigma
+// (a cube of xi) would carry it into the next iterate amplified.
+static double mu_grid(double x) {
+    static const double G[9] = {0x1.0000000000000p+0, 0x1.172b83c7d517bp+0, 0x1.306fe0a31b715p+0,
+                                0x1.4bfdad5362a27p+0, 0x1.6a09e667f3bcdp+0, 0x1.8ace5422aa0dbp+0,
+                                0x1.ae89f995ad3adp+0, 0x1.d5818dcfba487p+0, 0x1.0000000000000p+1};
+    static const double B[8] = {0x1.0b5586cf9890fp+0, 0x1.2387a6e756238p+0, 0x1.3dea64c123422p+0,
+                                0x1.5ab07dd485429p+0, 0x1.7a11473eb0187p+0, 0x1.9c49182a3f090p+0,
+                                0x1.c199bdd85529cp+0, 0x1.ea4afa2a490dap+0};
+    if (!(x > 0) || !std::isfinite(x)) return x;
+    int e;
+    const double y = 2.0 * std::frexp(x, &e);  // x = y 2^(e-1), y in [1, 2)
+    int j = 0;
+    for (int q = 0; q < 8; q++) j += y >= B[q];
+    return std::ldexp(G[j], e - 1);
+}
+
 // Cholesky of a dense n x n SPD matrix (row-major) with diagonal shift; returns false if not PD
 static bool chol_solve(const double* M, int n, double shift, const double* b, double* x) {
     double L[NMAX * NMAX];
@@ -75,21 +96,27 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
     std::vector<double> slo(R, 0), shi(R, 0), zlo(R, 0), zhi(R, 0);
     std::vector<double> dslo(R, 0), dshi(R, 0), dzlo(R, 0), dzhi(R, 0), rplo(R, 0), rphi(R, 0);
     double mu = opt.mu0;
-    for (int r = 0; r < R; r++) {
-        const double v = val(g, x, r);
-        double p = 0;
-        if (hlo[r] && hhi[r]) p = std::min(opt.bound_push * std::max(1.0, std::fabs(L[r])), opt.bound_push * (U[r] - L[r]));
-        if (hlo[r]) {
-            const double pl = hhi[r] ? p : opt.bound_push * std::max(1.0, std::fabs(L[r]));
-            slo[r] = std::max(v - L[r], pl);
-            zlo[r] = mu / slo[r];
+    // slacks pushed into the interior and multipliers mu / s at the current point (the start, and
+    // the restart after a successful restoration phase)
+    auto init_slacks = [&]() {
+        for (int r = 0; r < R; r++) {
+            const double v = val(g, x, r);
+            double p = 0;
+            if (hlo[r] && hhi[r]) p = std::min(opt.bound_push * std::max(1.0, std::fabs(L[r])), opt.bound_push * (U[r] - L[r]));
+            slo[r] = 0; zlo[r] = 0; shi[r] = 0; zhi[r] = 0;
+            if (hlo[r]) {
+                const double pl = hhi[r] ? p : opt.bound_push * std::max(1.0, std::fabs(L[r]));
+                slo[r] = std::max(v - L[r], pl);
+                zlo[r] = mu / slo[r];
+            }
+            if (hhi[r]) {
+                const double pu = hlo[r] ? p : opt.bound_push * std::max(1.0, std::fabs(U[r]));
+                shi[r] = std::max(U[r] - v, pu);
+                zhi[r] = mu / shi[r];
+            }
         }
-        if (hhi[r]) {
-            const double pu = hlo[r] ? p : opt.bound_push * std::max(1.0, std::fabs(U[r]));
-            shi[r] = std::max(U[r] - v, pu);
-            zhi[r] = mu / shi[r];
-        }
-    }
+    };
+    init_slacks();
 
     double H[NMAX * NMAX] = {0};
     for (int j = 0; j < n; j++) H[j * n + j] = 1.0;
@@ -104,10 +131,117 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
     // adaptive_mu_monotone_init_factor 0.8, mu_oracle loqo)
     bool free_mode = opt.mu_strategy == 1;
     std::vector<double> kkt_ref;
-    const double mu_min = 1e-11;
+    // the adaptive rule's floor: tol / 10, the monotone rule's floor (Ipopt's mu_min default is
+    // 1e-11; below ~tol / 10 the reduced system's Sigma = z / s ~ z^2 / mu of the active rows makes
+    // the 1e-4-tolerance solution reproducible to ~1e-5 only: DESIGN.md §5, tools/mu_sensitivity.py)
+    const double mu_min = (opt.mu_study & 2) ? 1e-11 : opt.tol / 10;
     IpmResult res{1, 0, 0, 0.0, 0.0};
     double a[NMAX], at[NMAX];
     int it;
+    int nresto = 0;
+    // Restoration phase (the device statement is nlp_kernels.hip resto_*). From the
+    // current x (g, J at x), Gauss-Newton steps on
+    //   Phi(x) = 1/2 sum_r e_r(x)^2 + mu_R sum_j (-ln(1 - x_j) - ln(1 + x_j)),
+    //   e_r = max(0, (L_r + delta) - g_r, g_r - (U_r - delta)) over the constraint rows' finite sides
+    // (targets delta inside the bounds, so a point that reaches them is strictly feasible; the box
+    // |x| < 1 by the barrier and the fraction to the boundary), Levenberg-Marquardt damping
+    // lambda = 1e-2 min(1, |e|_2) (1 + max_j M_jj), an Armijo backtracking search over max_ls
+    // halvings. Each iteration in order: (1) every original row within its bounds -> 0 (restart the
+    // interior point); (2) the iteration cap -> 1; (3) Phi decreased by at most resto_stall x Phi
+    // in two consecutive iterations -> 4 (local infeasibility); (4) the step, or 4 when the
+    // factorisation or the line search fails. Accepted steps count as iterations.
+    auto restoration = [&](int& iter, int& ne) -> int {
+        double phi_prev = -1;
+        int stall = 0;
+        for (;;) {
+            double Mr[NMAX * NMAX] = {0}, br[NMAX] = {0}, V = 0, e0max = 0;
+            for (int r = 0; r < m; r++) {
+                const double v = g[r];
+                double e = 0, sg = 0, e0 = 0;
+                if (hlo[r]) {
+                    e0 = std::max(e0, L[r] - v);
+                    const double el = (L[r] + opt.resto_delta) - v;
+                    if (el > 0) { e = el; sg = -1.0; }
+                }
+                if (hhi[r]) {
+                    e0 = std::max(e0, v - U[r]);
+                    const double eh = v - (U[r] - opt.resto_delta);
+                    if (e == 0 && eh > 0) { e = eh; sg = 1.0; }
+                }
+                e0max = std::max(e0max, e0);
+                if (e > 0) {
+                    grow(J, r, a);
+                    V += e * e;
+                    const double es = e * sg;
+                    for (int i = 0; i < n; i++) {
+                        br[i] += es * a[i];
+                        for (int j = 0; j < n; j++) Mr[i * n + j] += a[i] * a[j];
+                    }
+                }
+            }
+            if (e0max <= 0) return 0;
+            if (iter >= opt.max_iter) return 1;
+            auto barrier = [&](const double* xv) {
+                double b = 0;
+                for (int j = 0; j < n; j++) b += -std::log(1.0 - xv[j]) - std::log(1.0 + xv[j]);
+                return opt.resto_mu * b;
+            };
+            const double phi = 0.5 * V + barrier(x);
+            if (phi_prev >= 0) {
+                stall = (phi_prev - phi <= opt.resto_stall * phi_prev) ? stall + 1 : 0;
+                if (stall >= 2) return 4;
+            }
+            phi_prev = phi;
+            double dmax = 0;
+            for (int j = 0; j < n; j++) dmax = std::max(dmax, Mr[j * n + j]);
+            const double lam = 1e-2 * std::min(1.0, std::sqrt(V)) * (1.0 + dmax);
+            double A[NMAX * NMAX], rhs[NMAX], gp[NMAX], dxr[NMAX];
+            for (int i = 0; i < n * n; i++) A[i] = Mr[i];
+            for (int j = 0; j < n; j++) {
+                const double u = 1.0 - x[j], l = 1.0 + x[j];
+                gp[j] = br[j] + opt.resto_mu * (1.0 / u - 1.0 / l);
+                A[j * n + j] += opt.resto_mu * (1.0 / (u * u) + 1.0 / (l * l)) + lam;
+                rhs[j] = -gp[j];
+            }
+            double shift = 0.0;
+            bool ok = false;
+            for (int tries = 0; tries < 40 && !ok; tries++) {
+                ok = chol_solve(A, n, shift, rhs, dxr);
+                shift = (shift == 0.0) ? 1e-8 : shift * 10;
+            }
+            if (!ok) return 4;
+            double amax = 1.0, dphi = 0;
+            for (int j = 0; j < n; j++) {
+                if (dxr[j] > 0) amax = std::min(amax, opt.tau_min * (1.0 - x[j]) / dxr[j]);
+                if (dxr[j] < 0) amax = std::min(amax, opt.tau_min * (-1.0 - x[j]) / dxr[j]);
+                dphi += gp[j] * dxr[j];
+            }
+            double al = amax, xr[NMAX];
+            bool acc = false;
+            for (int ls = 0; ls < opt.max_ls && !acc; ls++) {
+                for (int j = 0; j < n; j++) xr[j] = x[j] + al * dxr[j];
+                prob.eval(xr, &ft, gradt, gt.data(), Jt.data());
+                ne++;
+                double Vt = 0;
+                for (int r = 0; r < m; r++) {
+                    const double v = gt[r];
+                    double e = 0;
+                    if (hlo[r]) { const double el = (L[r] + opt.resto_delta) - v; if (el > 0) e = el; }
+                    if (hhi[r]) { const double eh = v - (U[r] - opt.resto_delta); if (e == 0 && eh > 0) e = eh; }
+                    Vt += e * e;
+                }
+                const double phit = 0.5 * Vt + barrier(xr);
+                if (phit <= phi + opt.eta * al * dphi) acc = true;
+                else al *= 0.5;
+            }
+            if (!acc) return 4;
+            for (int j = 0; j < n; j++) { x[j] = xr[j]; grad[j] = gradt[j]; }
+            f = ft;
+            g.swap(gt);
+            J.swap(Jt);
+            iter++;
+        }
+    };
     for (it = 0; it < opt.max_iter; it++) {
         // 1. residuals and errors
         double rd[NMAX];
@@ -173,7 +307,7 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             const double mu_old = mu;
             if (free_mode && !progress) {
                 free_mode = false;
-                mu = std::max(mu_min, 0.8 * avg);
+                mu = std::max(mu_min, (opt.mu_study & 1) ? 0.8 * avg : mu_grid(0.8 * avg));
                 kkt_ref.assign(1, E0);
             } else if (!free_mode && progress && !kkt_ref.empty() && E0 <= 0.9999 * kkt_ref.back()) {
                 free_mode = true;
@@ -184,7 +318,7 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
                 if (kkt_ref.size() > 4) kkt_ref.erase(kkt_ref.begin());
                 const double xi = mn / avg;
                 const double sg = 0.1 * std::pow(std::min(0.05 * (1 - xi) / xi, 2.0), 3);
-                mu = std::max(mu_min, std::min(sg * avg, 1e5));
+                mu = std::max(mu_min, std::min((opt.mu_study & 1) ? sg * avg : mu_grid(sg * avg), 1e5));
             } else if (Emu <= opt.kappa_eps * mu && mu > opt.tol / 10) {
                 mu = std::max(opt.tol / 10, std::min(opt.kappa_mu * mu, std::pow(mu, opt.theta_mu)));
             }
@@ -293,6 +427,29 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             }
             if (ok) { accepted = true; break; }
             if (ls + 1 < opt.max_ls) alpha *= 0.5;
+        }
+        if (!accepted && nresto < opt.resto_max) {
+            // 5b. restoration phase (the role of Ipopt's, which it enters when the line search finds
+            //     no acceptable trial): minimise the constraint violation from x, then restart
+            nresto++;
+            it++;  // the failed iteration counts
+            const int rs = restoration(it, nevals);
+            if (rs == 1) { res.status = 1; break; }
+            if (rs == 4) { res.status = 4; break; }
+            // every row within its bounds: the interior point restarts at x (slacks and multipliers
+            // as at the start, at the current mu; a fresh filter and BFGS matrix)
+            init_slacks();
+            for (int i = 0; i < n * n; i++) H[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
+            first_update = true;
+            filt_theta.clear();
+            filt_phi.clear();
+            theta_max = -1;
+            theta_min = -1;
+            nfail = 0;
+            free_mode = opt.mu_strategy == 1;
+            kkt_ref.clear();
+            it--;  // (the loop's increment; restoration counted its own iterations)
+            continue;
         }
         if (accepted && !ftype) { filt_theta.push_back((1 - 1e-5) * theta0); filt_phi.push_back(phi0 - 1e-8 * theta0); }
         // a trial forced after max_ls halvings counts as a failed line search; three in a row end

@@ -36,14 +36,26 @@ struct IpmOptions {
     double kappa_sigma = 1e10;
     double s_max = 100.0;
     double inf_bound = 1e19;
-    // barrier strategy: 0 monotone (the build's solver, GPU and CPU); 1 adaptive (Ipopt's
-    // mu_strategy "adaptive", KPR/Parameters.h:57, with the LOQO mu oracle and the kkt-error
-    // globalisation, restated in ipm.cpp; an option, see DESIGN.md §5 for why it is not the default)
-    int mu_strategy = 0;
+    // barrier strategy: 1 adaptive (the default: the reference's IPOPT_MU_STRATEGY "adaptive",
+    // KPR/Parameters.h:57, restated with Ipopt's mu_oracle loqo and adaptive_mu_globalization
+    // kkt-error — not Ipopt's default quality-function / obj-constr-filter pair — with mu on a
+    // 2^(1/8) grid and the floor tol / 10; ipm.cpp); 0 monotone (Fiacco-McCormick)
+    int mu_strategy = 1;
+    // studies of the adaptive rule only (tools/mu_sensitivity.py): bit 0 drops the 2^(1/8) grid
+    // (ipm.cpp mu_grid), bit 1 the tol / 10 floor (Ipopt's mu_min 1e-11 instead)
+    int mu_study = 0;
+    // restoration phase (ipm.cpp restoration): phases per solve (0: none; a failed line search
+    // then takes the last trial, and three in a row end the solve), violation target inside the
+    // bounds, box barrier weight, stall ratio
+    int resto_max = 3;
+    double resto_delta = 1e-6;
+    double resto_mu = 1e-8;
+    double resto_stall = 1e-4;
 };
 
 struct IpmResult {
-    int status;        // 0 converged, 1 max_iter, 2 line-search failure
+    int status;        // 0 converged, 1 max_iter, 2 line-search failure, 4 local infeasibility
+                       // (the restoration phase stalled or failed; 3 is the ABI's "not planned")
     int iterations;
     int evaluations;
     double obj;

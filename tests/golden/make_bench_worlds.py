@@ -77,7 +77,8 @@ def main():
     st = rec["status"]
     summary = dict(worlds=N_WORLDS, T=T, O=O, profile=PROFILE, feasible=int(rec["feasible"].sum()),
                    converged=int((st == 0).sum()), iteration_cap=int((st == 1).sum()),
-                   line_search_failure=int((st == 2).sum()), mean_iterations=float(rec["iterations"].mean()),
+                   line_search_failure=int((st == 2).sum()), local_infeasibility=int((st == 4).sum()),
+                   mean_iterations=float(rec["iterations"].mean()),
                    seconds=round(time.time() - t0, 1))
     print(json.dumps(summary), flush=True)
     if cap_study:

@@ -47,7 +47,8 @@ def test_fixture_covers_the_workload():
     fx = load()
     st = fx["status"]
     assert 0.5 < fx["feasible"].mean() < 0.75          # ~62 % feasible: the solver works against active limits
-    assert (st == 0).sum() > 500 and (st == 2).sum() > 300
+    # infeasible worlds end in the restoration phase's local-infeasibility verdict (status 4)
+    assert (st == 0).sum() > 500 and (st == 4).sum() > 300
     # every converged plan is a KKT point to the reference's tolerance (IPOPT_OPTIMIZATION_TOLERANCE
     # 1e-4, KPR/Parameters.h:50), with the Ipopt scaling of the error (ipm.cpp)
     assert np.all(fx["kkt"][st == 0] <= 1e-4)
@@ -55,10 +56,10 @@ def test_fixture_covers_the_workload():
     assert np.all(fx["feasible"][st == 0])
 
 
-@pytest.mark.parametrize("i", [1, 5, 75, 300])
+@pytest.mark.parametrize("i", [1, 5, 55, 300])
 def test_oracle_reproduces_fixture_plans(i):
-    """converged (1), infeasible (5, 300) and iteration-limit (75) worlds re-planned"""
-    assert int(load()["status"][75]) == 1
+    """converged (1), infeasible (5, 300) and iteration-limit (55) worlds re-planned"""
+    assert int(load()["status"][55]) == 1
     fx = load()
     R = OraclePlanner(*bench_world(fx, i), T=int(fx["T"]), threads=8)
     R.reach()
@@ -70,10 +71,11 @@ def test_oracle_reproduces_fixture_plans(i):
 
 def test_cap_study_recorded():
     """the worlds that end at the 100-iteration cap, re-planned with Ipopt's default limit of 3000
-    (tests/golden/bench_cap_study.json): none becomes feasible, so the cap changes no decision"""
+    (tests/golden/bench_cap_study.json): every one keeps its verdict (the re-check at the final
+    iterate, KPR/NLPclass.cu:449-538), so the cap changes no decision"""
     rec = json.load(open(os.path.join(GOLD, "bench_cap_study.json")))
     fx = load()
     assert len(rec["worlds"]) == int((fx["status"] == 1).sum()) > 0
     for w in rec["worlds"]:
-        assert not w["cap100"]["feasible"] and not w["cap3000"]["feasible"]
+        assert w["cap100"]["feasible"] == w["cap3000"]["feasible"]
         assert w["cap3000"]["iterations"] < 3000

@@ -37,7 +37,7 @@ def test_copy_bandwidth():
     assert 1000 < gbs < 8000
 
 
-def _bench_two_ranks(extra):
+def _bench_two_ranks(extra, timeout=400):
     """bench.py under torch.distributed.run with two ranks sharing the box's one GPU (collectives on
     gloo: RCCL refuses two ranks on one device). Everything else is the N > 1 path the driver runs
     on an 8-GPU node: world sharding, barriers, max-over-ranks timing, the record all-gather and
@@ -48,7 +48,7 @@ def _bench_two_ranks(extra):
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
            "--warmup", "1", "--cpu-seconds", "0", "--no-extras"] + extra
     env = dict(os.environ, ARMOUR_DIST_BACKEND="gloo")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
@@ -66,3 +66,34 @@ def test_bench_two_ranks_weak_scaling():
     """the default (weak) mode at N = 2: each rank plans its own worlds, 2 x 16 per step"""
     line = _bench_two_ranks(["--batch", "16", "--planners", "1"])
     assert line["scaling"] == "weak" and line["total_worlds_last_step"] == 32
+
+
+def test_config4_256_worlds_two_ranks_match_oracle(tmp_path):
+    """BASELINE config 4 as specified: one job of 256 random-obstacle worlds (seeds 0..255 of the
+    headline generator) sharded over the ranks — here two ranks sharing the box's GPU, 128 worlds
+    each over the bench's three planners — and every gathered record compared with the oracle's
+    plan of the same seed (tests/golden/bench_survey_T100_O20.npz holds seeds 0..980): feasibility
+    and solver status identical for all 256, k_opt within 1e-8 for converged plans on the oracle's
+    path (the bench-worlds bar: at most 1 % of the worlds off it, test_gpu_bench_worlds.py)."""
+    import numpy as np
+    from armour_amd import dist as D
+    from test_bench_worlds import load
+
+    out = tmp_path / "config4_records.npy"
+    line = _bench_two_ranks(["--total-worlds", "256", "--dump-records", str(out)], timeout=600)
+    assert line["scaling"] == "strong" and line["total_worlds_last_step"] == 256
+    assert line["config"]["worlds_per_gpu"] == 128 and line["config"]["planners_per_gpu"] == 3
+    rec = np.load(out)
+    fx = load()
+    assert rec.shape == (256, D.RECORD)
+    feas, status = rec[:, 8] > 0.5, rec[:, 9].astype(int)
+    assert np.array_equal(feas, fx["feasible"][:256]), np.nonzero(feas != fx["feasible"][:256])[0]
+    assert np.array_equal(status, fx["status"][:256]), np.nonzero(status != fx["status"][:256])[0]
+    conv = status == 0
+    dk = np.abs(rec[:, :7] - fx["k_opt"][:256]).max(axis=1)
+    off = np.nonzero(conv & (dk > 1e-8))[0]
+    print(f"config 4: 256 worlds, {int(feas.sum())} feasible, converged k_opt within 1e-8: "
+          f"{int(conv.sum()) - len(off)}/{int(conv.sum())} (max {dk[conv].max():.1e}); best world {D.best(rec)}")
+    assert len(off) <= 256 // 100 and dk[conv].max() <= 1e-4
+    assert D.best(rec) == D.best(np.column_stack([fx["k_opt"][:256], fx["cost"][:256], fx["feasible"][:256],
+                                                  fx["status"][:256]])) or len(off) > 0

@@ -90,14 +90,49 @@ def test_infeasible_verdict_has_no_feasible_point(i):
     assert best > 1e-2  # above both thresholds (torque 1e-2, collision 1e-4)
 
 
-def test_adaptive_barrier_option():
-    """IPOPT_MU_STRATEGY is "adaptive" (KPR/Parameters.h:57); the build's default barrier is monotone
-    and the adaptive one (LOQO oracle) is an option. On bench world 235 the monotone
-    solve ends in line-search failure (infeasible) while the adaptive one converges to a feasible
-    plan: the one decision of the 400 compared worlds that differs (profiles/r03_mu_study.json)"""
+def test_world_235_false_infeasible_fixed():
+    """World 235 of the headline workload was round 3's one false -1 (tools/phase1_study.py: SLSQP
+    phase 1 found a point within every bound): r03's solver (monotone barrier, no restoration phase:
+    mu_strategy 0, flags 4) ends it in line-search failure; the default (the reference's adaptive
+    barrier, KPR/Parameters.h:57, and the restoration phase) plans it feasible"""
     fx = load()
     R = OraclePlanner(*bench_world(fx, 235), T=int(fx["T"]), threads=8)
     R.reach()
-    mono, adap = R.plan(), R.plan(mu_strategy=1)
-    assert not mono["feasible"] and mono["status"] == 2 and not bool(fx["feasible"][235])
-    assert adap["feasible"] and adap["status"] == 0
+    r03 = R.plan(mu_strategy=0, flags=4)
+    assert not r03["feasible"] and r03["status"] == 2
+    r = R.plan()
+    assert r["feasible"] and r["status"] == 0 and bool(fx["feasible"][235])
+
+
+def test_phase1_study_finds_no_false_infeasible_verdict():
+    """tests/golden/phase1_study.json (tools/phase1_study.py over the current fixture): for every
+    world the solver declares infeasible, SLSQP phase 1 from x = 0, the solver's last iterate and 3
+    random starts, strict and on finalize_solution's own region, found no point that passes the
+    re-check (KPR/NLPclass.cu:449-538)"""
+    import json
+    import os
+
+    fx = load()
+    rec = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "phase1_study.json")))
+    infeasible = [int(i) for i in np.nonzero(~fx["feasible"])[0]]
+    assert [w["world"] for w in rec["worlds"]] == infeasible, "study out of date: rerun tools/phase1_study.py"
+    assert rec["n_false_infeasible"] == 0, rec["false_infeasible"]
+    for w in rec["worlds"]:
+        assert len(w["runs"]) == 7 and not any(r["finalize_feasible"] for r in w["runs"])
+
+
+def test_restoration_phase_ends_infeasible_worlds_early():
+    """The restoration phase (oracle/src/ipm.cpp) on infeasible headline worlds: the
+    verdict is local infeasibility (status 4) instead of three forced steps (status 2), the plan
+    stays infeasible, and together they cost fewer evaluations (one world, 35, takes a second phase
+    after a restart and costs more)"""
+    fx = load()
+    ev, ev_no = 0, 0
+    for i in INFEASIBLE:
+        R = OraclePlanner(*bench_world(fx, i), T=int(fx["T"]), threads=8)
+        R.reach()
+        r, no = R.plan(), R.plan(flags=4)
+        assert not r["feasible"] and not no["feasible"]
+        assert r["status"] == 4 and no["status"] == 2
+        ev, ev_no = ev + r["evaluations"], ev_no + no["evaluations"]
+    assert ev < ev_no
