@@ -141,6 +141,40 @@ def traffic_record(T, O, batch, profile):
     return best
 
 
+def rocprof_record(kernel="lane_reach_kernel"):
+    """The kernel's rocprofv3 --kernel-trace --stats line from the newest committed summary of the
+    same library build (profiles/r*_kernel_stats.txt written by tools/gpu.sh stats, whose header
+    names the library's SHA-1): (file, calls, average ns, min ns), or None"""
+    import glob
+
+    digest, best = lib_digest(), None
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats.txt"))):
+        lines = open(fn).read().splitlines()
+        if not any(ln.startswith("# lib_sha1 ") and ln.split()[2] == digest for ln in lines):
+            continue
+        for ln in lines:
+            if kernel in ln and not ln.startswith("#"):
+                f = ln[72:].split()
+                best = (fn, int(f[0]), float(f[2]), float(f[3]))
+                break
+    return best
+
+
+def io_lower_bound(P, W, nsample=16):
+    """Design-independent lower bound of the reach phase's HBM bytes per launch: every job reads its
+    7 JRS joint records (reach.h JrsJoint, 13 doubles) and writes only what the solver consumes — per
+    link the centre, radius and 3 x 6 generators and its k-only monomials (u16 hash + 3 doubles), per
+    joint the torque centre, radius and monomials (u16 + double) and the torque radius
+    (KPR/armour_main.cu:114-211). Intermediates kept on chip cost nothing here."""
+    T, NJ = P.T, P.NJ
+    tot = 0.0
+    n = min(nsample, W)
+    for w in range(n):
+        lk, tq = P.monomial_counts(w)
+        tot += T * (7 * 13 * 8 + NJ * 24 * 8 + 7 * 3 * 8) + 26 * float(lk.sum()) + 10 * float(tq.sum())
+    return tot / n * W
+
+
 def latency(A, O, robot, geo):
     """the drop-in's use: one world per call (KSI/uarmtd_planner.m runs one armour_main per plan)"""
     out = {}
@@ -420,6 +454,20 @@ def main():
                 "iterations_at_3000": [int(r["iterations"]) for r in long_res],
                 "status_at_3000": [int(r["status"]) for r in long_res],
                 "cost_delta": [float(r["cost"] - res[i]["cost"]) for r, i in zip(long_res, capped)]}
+        lb = io_lower_bound(planners[0], len(subs[0]))
+        line["roofline"]["io_lower_bound"] = {
+            "bytes_per_launch": lb, "frac": lb / (rk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "note": "design-independent: JRS scalars in, link and torque tables out (bench.py io_lower_bound); "
+                    "the kernel's own arena traffic is the algorithmic figure above"}
+        rp = rocprof_record() if a.robot == "kinova" else None
+        if rp is not None:
+            fn, calls, avg_ns, min_ns = rp
+            line["roofline"]["rocprof"] = {
+                "source": os.path.relpath(fn, ROOT), "calls": calls, "avg_ms": avg_ns * 1e-6, "min_ms": min_ns * 1e-6,
+                "frac_avg": rk_bytes / (avg_ns * 1e-9) / 1e9 / HBM_PEAK_GBS,
+                "frac_min": rk_bytes / (min_ns * 1e-9) / 1e9 / HBM_PEAK_GBS,
+                "note": "rocprofv3 --kernel-trace --stats of this bench command on the same library build: the average "
+                        "spans the timed region's launches under three planners and the solo launch"}
         tr = traffic_record(a.T, a.O, len(subs[0]), a.profile) if a.robot == "kinova" else None
         if tr is not None:
             line["roofline"]["traffic"] = tr[1]["traffic_bytes_per_launch"]

@@ -50,7 +50,9 @@ for step in "$@"; do
       (cd /tmp && env "${envs[@]}" timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
           -d "$OUT/$tag" -o run -- python3 "$R/$1" "${@:2}") > "$OUT/$tag.log" 2>&1
       rc=$?
-      [ $rc -eq 0 ] && python3 tools/stats_summary.py "$OUT/$tag/run_kernel_stats.csv" "$OUT/$tag.txt" "$step" && head -14 "$OUT/$tag.txt" ;;
+      [ $rc -eq 0 ] && python3 tools/stats_summary.py "$OUT/$tag/run_kernel_stats.csv" "$OUT/$tag.txt" "$step" \
+          "lib_sha1 $(python3 -c 'import hashlib; print(hashlib.sha1(open("armour-dev_amd/armour_amd/libarmour_hip.so","rb").read()).hexdigest()[:16])')" \
+          && head -14 "$OUT/$tag.txt" ;;
     pmc)
       ctrs=$1; shift
       prog=(python3 "$R/$1"); [[ "$1" == *.py ]] || prog=("$R/$1")
