@@ -141,6 +141,7 @@ struct NlpDev {
     // restoration launches: the trial and full evaluations take the worlds in the restoration
     // phase (status WS_RESTO) instead of the searching ones
     int resto;
+    int rflag;              // mapped host flag that resto_world_G's count goes to
     // Certified plane cache (plane_cache_kernel). The 36 planes of a buffered
     // obstacle and their offsets d, delta do not depend on x; only A . c(x) does. For every
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in

@@ -652,7 +652,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
     WorldState& S = d.ws[w];
     // (restoration launches, d.resto: the worlds in the restoration phase, WS_RESTO)
     if (mode == 1 && !((d.resto ? S.status == WS_RESTO : S.status == 0) && S.searching)) return;
-    if (mode == 5 && !(S.status == 0 && S.spec_k >= 0)) return;
+    if (mode == 5 && !(d.resto ? (S.status == WS_RESTO && S.rpend) : (S.status == 0 && S.spec_k >= 0))) return;
     const int slot = mode == 0 ? 0 : 1 - S.cur;
     double* const Gb = d.g + gidx(d, slot, w, 0);
     double* const Jb = d.J + gidx(d, slot, w, 0) * NF;
@@ -1155,7 +1155,8 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     if (d.lcount && blockIdx.y >= *d.lcount) return;
     const int t = blockIdx.x, i = blockIdx.y, w = d.wl[i];
     const WorldState& S = d.ws[w];
-    if (!(S.status == 0 && (d.b_in_cs || S.searching))) return;
+    // (restoration launches, d.resto: the trials of the phase's Armijo search)
+    if (!(d.resto ? (S.status == WS_RESTO && S.searching) : (S.status == 0 && (d.b_in_cs || S.searching)))) return;
     const RobotParams& rp = *d.rp;
     const int tid = threadIdx.x, K = d.K;
     const long jt = (long)w * d.T + t;
@@ -2421,7 +2422,7 @@ __global__ __launch_bounds__(64) void resto_world_G(NlpDev d) {
     }
     __syncthreads();
     ws_copy(d.ws[w], S);
-    if (threadIdx.x == 0) resto_count(d, S.status == WS_RESTO, 0);
+    if (threadIdx.x == 0) resto_count(d, S.status == WS_RESTO, d.rflag);
 }
 
 // sum e^2 at the trial point (the trial slot's full evaluation, mode 1)
@@ -2476,6 +2477,77 @@ __global__ __launch_bounds__(64) void resto_world_V(NlpDev d) {
     __syncthreads();
     ws_copy(d.ws[w], S);
     if (threadIdx.x == 0) resto_count(d, S.status == WS_RESTO && S.searching, 1);
+}
+
+// The phase's Armijo search in one round (planner.hip run_resto, when the speculative machinery is
+// there): the values of all max_ls trials (eval_trials_all, d.resto) summed per trial
+// (resto_rows_Vs, list entry i and trial k at blockIdx.y = i K + k, the rows and partial sums of
+// resto_rows_V), the tests in trial order (resto_world_Vs), then the chosen trial in full (eval
+// mode 5, d.resto). The decisions and the chosen point are those of the sequential rounds.
+__global__ __launch_bounds__(ROW_THREADS) void resto_rows_Vs(NlpDev d) {
+    const int i = blockIdx.y / d.K;
+    const int w = d.wl[i];
+    const WorldState& S = d.ws[w];
+    if (!(S.status == WS_RESTO && S.searching)) return;
+    __shared__ double lds[(ROW_THREADS / 64) * NRG];
+    const double* G = d.gs + (long)blockIdx.y * d.m;
+    double V = 0;
+    const long r0 = (long)blockIdx.x * d.chunk, wb = (long)w * d.R;
+    for (long r = r0 + threadIdx.x; r < r0 + d.chunk && r < d.m; r += blockDim.x) {
+        const long ii = wb + r;
+        const RowBounds B(d, ii, wb, (int)r);
+        double e, sg, e0;
+        resto_row(d, G[r], B.L(), B.U(), e, sg, e0);
+        V += e * e;
+    }
+    double vv[1] = {V};
+    const int kinds[1] = {0};
+    block_reduce_n(vv, kinds, lds, d.partial_s + ((long)blockIdx.y * d.nblk + blockIdx.x) * KA);
+}
+__global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
+    const int i = blockIdx.x, w = d.wl[i];
+    __shared__ WorldState S;
+    ws_copy(S, d.ws[w]);
+    __syncthreads();
+    if (S.status == WS_RESTO && S.searching) {
+        // trial k's sum on lane k, its blocks combined in order (world_partials_at's arithmetic)
+        const int lane = threadIdx.x & 63;
+        double v = 0.0;
+        if (lane < d.K) {
+            const double* in = d.partial_s + ((long)i * d.K + lane) * d.nblk * KA;
+            for (int b0 = 0; b0 < d.nblk; b0 += 16) {
+                double xb[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) xb[u] = in[(long)min(b0 + u, d.nblk - 1) * KA];
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    if (b0 + u < d.nblk) v = v + xb[u];
+            }
+        }
+        const uint64_t u = __builtin_bit_cast(uint64_t, v);
+        for (int k = 0; k < d.K; k++) {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+            const double Vk = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+            if (threadIdx.x == 0 && S.searching) {
+                // resto_world_V's test of trial k (S.xt, S.alpha are trial k's)
+                S.nevals++;
+                const double phit = 0.5 * Vk + resto_barrier(d, S.xt);
+                if (phit <= S.phi0 + d.opt.eta * S.alpha * S.Dphi) {
+                    S.searching = 0;
+                    S.rpend = 1;
+                } else if (++S.ls >= d.opt.max_ls) {
+                    S.searching = 0;
+                    S.status = 5;
+                } else {
+                    S.alpha *= 0.5;
+                    for (int j = 0; j < NF; j++) S.xt[j] = S.x[j] + S.alpha * S.dx[j];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    ws_copy(d.ws[w], S);
 }
 
 // the worlds of list `in` (n entries; null: worlds 0..n-1) with status `st`, into `out`; the count

@@ -111,6 +111,7 @@ struct armour_planner {
     int* d_lists = nullptr;   // [4][max_worlds] active-world lists of the solver
     bool spec = true;         // speculative line-search rounds (ARMOUR_NO_SPEC: sequential only)
     bool spec_all = true;     // the sync-free tail's one-round line search (eval_trials_all, ipm_world_Cs_all)
+    bool resto_spec = false;  // the restoration phase's one-round search (eval_trials_all, resto_world_Vs)
     int tail_search = 1;      // its use (ARMOUR_TAIL_SEARCH): 0 rounds only, 1 adaptive, 2 always
     WorldState* h_ws = nullptr;
     double* h_f = nullptr;
@@ -468,9 +469,13 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // The sync-free tail may search all max_ls trials of its (at most tail_worlds) running worlds in
     // one round (run_solver)
     p->spec_all = p->spec && p->tail_search > 0 && (d.K + 1) * NJ * Om <= UB_FULL;
+    // the restoration phase searches all max_ls trials of up to every world at once
+    p->resto_spec = p->spec && d.opt.resto_max > 0 && d.opt.max_ls <= EV_MAXK + 1 && d.opt.max_ls * NJ * Om <= UB_FULL &&
+                    !std::getenv("ARMOUR_RESTO_ROUNDS");
     if (p->spec) {
         const size_t nall = p->spec_all ? (size_t)std::min(Wm, std::max(p->tail_worlds, 0)) * (d.K + 1) : 0;
-        const size_t ns = std::max((size_t)Wm * d.K, nall);
+        const size_t nres = p->resto_spec ? (size_t)Wm * d.opt.max_ls : 0;
+        const size_t ns = std::max(std::max((size_t)Wm * d.K, nall), nres);
         if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.fs, ns)) || (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
             return rc;
     }
@@ -901,17 +906,45 @@ static int ipm_loop(armour_planner* p, int nrun) {
 }
 
 // One restoration phase for the n worlds of `list` (status WS_RESTO), all together: per iteration
-// the Gauss-Newton pass and world step, then the Armijo search one trial per round (a full
-// evaluation into the trial slot each; rounds after the first are launched without a host
-// synchronisation, their blocks exit for worlds that stopped searching). The worlds leave with
-// status 0 (every row within its bounds: restart), 2 (iteration cap) or 5 (local infeasibility).
+// the Gauss-Newton pass and world step, then the Armijo search. With the speculative machinery
+// (p->resto_spec) the search is one round — the values of all max_ls trials, their sums, the tests
+// in trial order and the chosen trial's full evaluation — and iterations are launched without a
+// host synchronisation: the host reads iteration k - 1's count of worlds still in the phase (mapped
+// flags[2 + (k - 1) & 1], written by resto_world_G) after launching iteration k, so at most one
+// empty iteration is launched. Otherwise one trial per round (a full evaluation each; rounds after
+// the first launched without a synchronisation, their blocks exit for worlds that stopped). The
+// worlds leave with status 0 (every row within its bounds: restart), 2 (iteration cap) or 5 (local
+// infeasibility). Either way the arithmetic and decisions are the oracle's sequential ones.
 static int run_resto(armour_planner* p, const int* list, int n) {
     NlpDev dr = p->d;
     dr.wl = list;
     dr.resto = 1;
     dr.lcount = nullptr;
+    dr.b_in_cs = 0;
     const volatile int* fl = p->h_flags;
-    for (int guard = 0; guard < 4 * (dr.opt.max_iter + 1); guard++) {
+    const int guard = 4 * (dr.opt.max_iter + 1);
+    if (p->resto_spec) {
+        dr.K = dr.opt.max_ls;
+        for (int k = 0; k < guard; k++) {
+            dr.rflag = 2 + (k & 1);
+            hipLaunchKernelGGL(resto_rows_G, dim3(dr.nblk, n), dim3(ROW_THREADS), 0, p->stream, dr);
+            hipLaunchKernelGGL(resto_world_G, dim3(n), dim3(64), 0, p->stream, dr);
+            hipLaunchKernelGGL(eval_trials_all, dim3(p->T, n), dim3(EVAL_THREADS), 0, p->stream, dr);
+            hipLaunchKernelGGL(resto_rows_Vs, dim3(dr.nblk, n * dr.K), dim3(ROW_THREADS), 0, p->stream, dr);
+            hipLaunchKernelGGL(resto_world_Vs, dim3(n), dim3(64), 0, p->stream, dr);
+            launch_eval(p, dim3(p->T, n), dr, 5);
+            HIPCK(hipEventRecord(p->tev[k & 1], p->stream));
+            HIPCK(hipGetLastError());
+            if (k > 0) {
+                HIPCK(hipEventSynchronize(p->tev[(k - 1) & 1]));
+                if (fl[2 + ((k - 1) & 1)] == 0) break;  // iteration k - 1 found no world in the phase
+            }
+        }
+        HIPCK(hipStreamSynchronize(p->stream));
+        return 0;
+    }
+    dr.rflag = 0;
+    for (int k = 0; k < guard; k++) {
         hipLaunchKernelGGL(resto_rows_G, dim3(dr.nblk, n), dim3(ROW_THREADS), 0, p->stream, dr);
         hipLaunchKernelGGL(resto_world_G, dim3(n), dim3(64), 0, p->stream, dr);
         HIPCK(hipStreamSynchronize(p->stream));

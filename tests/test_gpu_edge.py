@@ -116,6 +116,32 @@ def test_speculative_line_search_matches_sequential():
         assert np.array_equal(g_s[w], Q.constraints(w)) and np.array_equal(c_s[w], Q.link_centers(w))
 
 
+def test_restoration_one_round_matches_rounds():
+    """The restoration phase's one-round Armijo search (all max_ls trials' values at once, iterations
+    launched without a host synchronisation; planner.hip run_resto) gives bitwise the plans of the
+    phase's sequential rounds (ARMOUR_RESTO_ROUNDS), on full-range worlds a third of which end in
+    local infeasibility (status 4) and some of which restart the interior point"""
+    import os
+
+    T, O = 40, 10
+    worlds = [A.make_world(s, O, profile="survey") for s in range(64)]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
+    res_s, _ = P.plan(worlds)
+    g_s = [P.constraints(w) for w in range(len(worlds))]
+    os.environ["ARMOUR_RESTO_ROUNDS"] = "1"
+    try:
+        Q = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
+    finally:
+        del os.environ["ARMOUR_RESTO_ROUNDS"]
+    res_q, _ = Q.plan(worlds)
+    assert sum(r["status"] == 4 for r in res_q) >= 8, "too few worlds in the restoration phase"
+    for w, (a, b) in enumerate(zip(res_s, res_q)):
+        assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"]
+        assert (a["iterations"], a["evaluations"], a["status"], a["feasible"]) == \
+            (b["iterations"], b["evaluations"], b["status"], b["feasible"])
+        assert np.array_equal(g_s[w], Q.constraints(w))
+
+
 @pytest.mark.parametrize("search", ["adaptive", "one", "rounds"])
 @pytest.mark.parametrize("tail", ["1000", "16"])
 def test_sync_free_tail_matches_synchronised(tail, search):
