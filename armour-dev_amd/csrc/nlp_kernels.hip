@@ -2273,6 +2273,7 @@ __device__ inline double resto_barrier(const NlpDev& d, const double* x) {
 }
 
 __global__ __launch_bounds__(ROW_THREADS) void resto_rows_G(NlpDev d) {
+    if (d.lcount && blockIdx.y >= *d.lcount) return;
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != WS_RESTO) return;
@@ -2400,6 +2401,7 @@ __device__ inline void resto_count(const NlpDev& d, bool mine, int flag) {
 }
 
 __global__ __launch_bounds__(64) void resto_world_G(NlpDev d) {
+    if (d.lcount && blockIdx.x >= *d.lcount) return;  // (one-round search: no count published)
     const int w = world_of(d, blockIdx.x);
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
@@ -2422,7 +2424,7 @@ __global__ __launch_bounds__(64) void resto_world_G(NlpDev d) {
     }
     __syncthreads();
     ws_copy(d.ws[w], S);
-    if (threadIdx.x == 0) resto_count(d, S.status == WS_RESTO, d.rflag);
+    if (threadIdx.x == 0 && d.rflag >= 0) resto_count(d, S.status == WS_RESTO, d.rflag);
 }
 
 // sum e^2 at the trial point (the trial slot's full evaluation, mode 1)
@@ -2486,6 +2488,7 @@ __global__ __launch_bounds__(64) void resto_world_V(NlpDev d) {
 // mode 5, d.resto). The decisions and the chosen point are those of the sequential rounds.
 __global__ __launch_bounds__(ROW_THREADS) void resto_rows_Vs(NlpDev d) {
     const int i = blockIdx.y / d.K;
+    if (d.lcount && (unsigned)i >= *d.lcount) return;
     const int w = d.wl[i];
     const WorldState& S = d.ws[w];
     if (!(S.status == WS_RESTO && S.searching)) return;
@@ -2504,12 +2507,18 @@ __global__ __launch_bounds__(ROW_THREADS) void resto_rows_Vs(NlpDev d) {
     const int kinds[1] = {0};
     block_reduce_n(vv, kinds, lds, d.partial_s + ((long)blockIdx.y * d.nblk + blockIdx.x) * KA);
 }
+// ... and the list compaction of the one-round iterations: the worlds still in the phase go to the
+// next iteration's list (wl_run), whose length the last block stores for the next launches (lrun_out,
+// device) and for the host (nrun_flag, mapped; read one iteration late)
 __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
-    const int i = blockIdx.x, w = d.wl[i];
+    const bool valid = !d.lcount || blockIdx.x < *d.lcount;
+    const int i = blockIdx.x, w = valid ? d.wl[i] : 0;
     __shared__ WorldState S;
-    ws_copy(S, d.ws[w]);
-    __syncthreads();
-    if (S.status == WS_RESTO && S.searching) {
+    if (valid) {
+        ws_copy(S, d.ws[w]);
+        __syncthreads();
+    }
+    if (valid && S.status == WS_RESTO && S.searching) {
         // trial k's sum on lane k, its blocks combined in order (world_partials_at's arithmetic)
         const int lane = threadIdx.x & 63;
         double v = 0.0;
@@ -2546,8 +2555,21 @@ __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
             }
         }
     }
-    __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (valid) {
+        __syncthreads();
+        ws_copy(d.ws[w], S);
+    }
+    if (threadIdx.x != 0) return;
+    if (valid && S.status == WS_RESTO) d.wl_run[atomicAdd(&d.cnt[0], 1u)] = w;
+    __threadfence();
+    if (atomicAdd(&d.cnt[2], 1u) == gridDim.x - 1) {
+        __threadfence();
+        const unsigned n = atomicAdd(&d.cnt[0], 0u);
+        *d.lrun_out = n;
+        *d.nrun_flag = (int)n;
+        d.cnt[0] = 0;
+        d.cnt[2] = 0;
+    }
 }
 
 // the worlds of list `in` (n entries; null: worlds 0..n-1) with status `st`, into `out`; the count

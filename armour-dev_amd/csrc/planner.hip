@@ -924,26 +924,41 @@ static int run_resto(armour_planner* p, const int* list, int n) {
     const volatile int* fl = p->h_flags;
     const int guard = 4 * (dr.opt.max_iter + 1);
     if (p->resto_spec) {
+        // iteration k works on list L[k & 1] (the first: `list`, n entries); resto_world_Vs appends
+        // the worlds still in the phase to L[(k + 1) & 1] and stores its length in cnt[8 + ((k + 1) & 1)]
+        // (the next launches' lcount) and flags[2 + (k & 1)] (read by the host after iteration k + 1
+        // is launched: the grid bound of iteration k + 2, or the end)
+        int* L[2] = {const_cast<int*>(list), p->d_lists + 3 * p->Wmax};
         dr.K = dr.opt.max_ls;
+        dr.rflag = -1;
+        int nb = n;  // grid bound: the last count the host knows (counts only fall)
         for (int k = 0; k < guard; k++) {
-            dr.rflag = 2 + (k & 1);
-            hipLaunchKernelGGL(resto_rows_G, dim3(dr.nblk, n), dim3(ROW_THREADS), 0, p->stream, dr);
-            hipLaunchKernelGGL(resto_world_G, dim3(n), dim3(64), 0, p->stream, dr);
-            hipLaunchKernelGGL(eval_trials_all, dim3(p->T, n), dim3(EVAL_THREADS), 0, p->stream, dr);
-            hipLaunchKernelGGL(resto_rows_Vs, dim3(dr.nblk, n * dr.K), dim3(ROW_THREADS), 0, p->stream, dr);
-            hipLaunchKernelGGL(resto_world_Vs, dim3(n), dim3(64), 0, p->stream, dr);
-            launch_eval(p, dim3(p->T, n), dr, 5);
+            NlpDev di = dr;
+            di.wl = L[k & 1];
+            di.wl_run = L[(k + 1) & 1];
+            di.lcount = k == 0 ? nullptr : p->d.cnt + 8 + (k & 1);
+            di.lrun_out = p->d.cnt + 8 + ((k + 1) & 1);
+            di.nrun_flag = p->d.flags + 2 + (k & 1);
+            hipLaunchKernelGGL(resto_rows_G, dim3(dr.nblk, nb), dim3(ROW_THREADS), 0, p->stream, di);
+            hipLaunchKernelGGL(resto_world_G, dim3(nb), dim3(64), 0, p->stream, di);
+            hipLaunchKernelGGL(eval_trials_all, dim3(p->T, nb), dim3(EVAL_THREADS), 0, p->stream, di);
+            hipLaunchKernelGGL(resto_rows_Vs, dim3(dr.nblk, nb * dr.K), dim3(ROW_THREADS), 0, p->stream, di);
+            hipLaunchKernelGGL(resto_world_Vs, dim3(nb), dim3(64), 0, p->stream, di);
+            launch_eval(p, dim3(p->T, nb), di, 5);
             HIPCK(hipEventRecord(p->tev[k & 1], p->stream));
             HIPCK(hipGetLastError());
             if (k > 0) {
                 HIPCK(hipEventSynchronize(p->tev[(k - 1) & 1]));
-                if (fl[2 + ((k - 1) & 1)] == 0) break;  // iteration k - 1 found no world in the phase
+                const int prev = fl[2 + ((k - 1) & 1)];  // worlds iteration k was launched for
+                if (prev == 0) break;
+                nb = prev < nb ? prev : nb;
             }
         }
         HIPCK(hipStreamSynchronize(p->stream));
         return 0;
     }
     dr.rflag = 0;
+    dr.lrun_out = nullptr;
     for (int k = 0; k < guard; k++) {
         hipLaunchKernelGGL(resto_rows_G, dim3(dr.nblk, n), dim3(ROW_THREADS), 0, p->stream, dr);
         hipLaunchKernelGGL(resto_world_G, dim3(n), dim3(64), 0, p->stream, dr);
@@ -989,7 +1004,8 @@ static int run_solver(armour_planner* p) {
         const int nr = fl[0];
         if (nr == 0) break;
         if ((rc = run_resto(p, Lr, nr))) break;
-        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)Lr, nr, 0, Li0, 0);
+        // the restarted worlds: after the loop only they can be running (the phase reorders its lists)
+        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, 0, Li0, 0);
         HIPCK(hipStreamSynchronize(p->stream));
         const int ni = fl[0];
         if (ni == 0) break;
