@@ -1923,7 +1923,7 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_C(NlpDev d) {
     block_reduce_n(v, kinds, lds, out);
 }
 
-__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft, bool filt);
+__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft, bool filt, int w);
 // the filter test of a trial (theta_t, phi_t) on a whole wave, one filter entry per lane
 // (MAX_FILTER <= 64): acceptable to the filter iff no entry dominates it
 __device__ inline bool filter_pass(const WorldState& S, double thetat, double phit) {
@@ -1940,12 +1940,12 @@ __device__ inline void world_C_body(const NlpDev& d, WorldState& S, int w) {
     const double ft = d.f[(1 - S.cur) * d.W + w];
     const bool filt = filter_pass(S, P[1], ft - S.mu * P[0]);
     if (threadIdx.x != 0) return;
-    accept_trial(d, S, P[0], P[1], ft, filt);
+    accept_trial(d, S, P[0], P[1], ft, filt, w);
 }
 
 // the filter acceptance test of one trial point (barrier terms logt, violation rpt, objective ft);
 // on failure the next trial (alpha halved) or, after max_ls trials, the forced last one
-__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft, bool filt) {
+__device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt, double rpt, double ft, bool filt, int w) {
     S.nevals++;
     const double phit = ft - S.mu * logt, thetat = rpt;
     bool ok = thetat <= S.theta_max && filt;  // filt: filter_pass of (thetat, phit)
@@ -1983,6 +1983,7 @@ __device__ inline void accept_trial(const NlpDev& d, WorldState& S, double logt,
             S.rphi = -1;
             S.rstall = 0;
             S.rpend = 0;
+            if (d.rl_app) d.rl_app[atomicAdd(&d.cnt[12], 1u)] = w;  // the loop's phase list
         }
         return;
     }
@@ -2139,7 +2140,7 @@ __device__ inline void world_Cs_body(const NlpDev& d, WorldState& S, int i) {
         // (the filter does not change while a search goes on: an acceptance ends it)
         const bool filt = filter_pass(S, rpt, ft - mu * logt);
         if (threadIdx.x == 0 && chosen == k - 1 && S.status == 0 && S.searching) {
-            accept_trial(d, S, logt, rpt, ft, filt);
+            accept_trial(d, S, logt, rpt, ft, filt, d.wl[i]);
             chosen = k;
         }
     }
@@ -2560,6 +2561,10 @@ __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
         ws_copy(d.ws[w], S);
     }
     if (threadIdx.x != 0) return;
+    if (d.rl_app) {  // inside the interior-point loop: the phase list, published by resto_publish
+        if (valid && S.status == WS_RESTO) d.rl_app[atomicAdd(&d.cnt[12], 1u)] = w;
+        return;
+    }
     if (valid && S.status == WS_RESTO) d.wl_run[atomicAdd(&d.cnt[0], 1u)] = w;
     __threadfence();
     if (atomicAdd(&d.cnt[2], 1u) == gridDim.x - 1) {
@@ -2570,6 +2575,15 @@ __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
         d.cnt[0] = 0;
         d.cnt[2] = 0;
     }
+}
+
+// the phase list's length (the worlds appended since the last publish: failed line searches of the
+// loop's last iteration and the worlds resto_world_Vs kept) for the phase iteration about to run:
+// cnt[14 + par] (its launches' lcount) and the mapped flags[6 + par] (the host, for grid bounds)
+__global__ void resto_publish(NlpDev d, int par) {
+    const unsigned n = atomicExch(&d.cnt[12], 0u);
+    d.cnt[14 + par] = n;
+    d.flags[6 + par] = (int)n;
 }
 
 // the worlds of list `in` (n entries; null: worlds 0..n-1) with status `st`, into `out`; the count

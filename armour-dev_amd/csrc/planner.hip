@@ -108,10 +108,11 @@ struct armour_planner {
     NlpDev d;
     int* feas = nullptr;
     int* h_flags = nullptr;   // pinned host, mapped (NlpDev::flags)
-    int* d_lists = nullptr;   // [4][max_worlds] active-world lists of the solver
+    int* d_lists = nullptr;   // [6][max_worlds] active-world lists of the solver
     bool spec = true;         // speculative line-search rounds (ARMOUR_NO_SPEC: sequential only)
     bool spec_all = true;     // the sync-free tail's one-round line search (eval_trials_all, ipm_world_Cs_all)
     bool resto_spec = false;  // the restoration phase's one-round search (eval_trials_all, resto_world_Vs)
+    bool resto_inline = true; // restoration phases inside the interior-point loop (ARMOUR_RESTO_INLINE=0: after it)
     int tail_search = 1;      // its use (ARMOUR_TAIL_SEARCH): 0 rounds only, 1 adaptive, 2 always
     WorldState* h_ws = nullptr;
     double* h_f = nullptr;
@@ -450,10 +451,11 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         return rc;
     // the solver's two continue flags live in mapped host memory: kernels store 1 into them, the
     // host clears and reads them between synchronised rounds (no fill or copy per round)
-    HIPCK(hipHostMalloc((void**)&p->h_flags, 6 * sizeof(int), hipHostMallocMapped));
+    HIPCK(hipHostMalloc((void**)&p->h_flags, 8 * sizeof(int), hipHostMallocMapped));
     HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
     // active-world lists: two per iteration (ping-pong), two per line-search round
-    if ((rc = p->alloc(&p->d_lists, 4 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 12))) return rc;
+    // (+ two for the restoration phases inside the interior-point loop)
+    if ((rc = p->alloc(&p->d_lists, 6 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 16))) return rc;
     // certified plane cache: room for all 36 planes of every (link, obstacle) pair of every (world, t)
     d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
     d.pcready = 0;
@@ -472,6 +474,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // the restoration phase searches all max_ls trials of up to every world at once
     p->resto_spec = p->spec && d.opt.resto_max > 0 && d.opt.max_ls <= EV_MAXK + 1 && d.opt.max_ls * NJ * Om <= UB_FULL &&
                     !std::getenv("ARMOUR_RESTO_ROUNDS");
+    p->resto_inline = p->resto_spec && !(std::getenv("ARMOUR_RESTO_INLINE") && std::atoi(std::getenv("ARMOUR_RESTO_INLINE")) == 0);
     if (p->spec) {
         const size_t nall = p->spec_all ? (size_t)std::min(Wm, std::max(p->tail_worlds, 0)) * (d.K + 1) : 0;
         const size_t nres = p->resto_spec ? (size_t)Wm * d.opt.max_ls : 0;
@@ -479,7 +482,8 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.fs, ns)) || (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
             return rc;
     }
-    HIPCK(hipMemset(d.cnt, 0, 12 * sizeof(unsigned)));
+    HIPCK(hipMemset(d.cnt, 0, 16 * sizeof(unsigned)));
+    d.rl_app = nullptr;
     d.lcount = nullptr;
     d.b_in_cs = 0;
     d.bt_flag = nullptr;
@@ -746,6 +750,43 @@ static int ipm_loop(armour_planner* p, int nrun) {
     int* Li[2] = {p->d_lists, p->d_lists + p->Wmax};                  // worlds of an iteration
     int* Ls[2] = {p->d_lists + 2 * p->Wmax, p->d_lists + 3 * p->Wmax};  // worlds of a line-search round
     const int ns = nside_count(p);
+    // Restoration phases inside the loop (with the speculative machinery): after each iteration's
+    // interior-point launches, one phase iteration (run_resto's one-round form) for the worlds whose
+    // line search failed so far and are still in their phase. Iteration it's failures (accept_trial)
+    // and the worlds phase iteration it - 1 kept are appended to RL[it & 1]; resto_publish hands its
+    // length to phase iteration it, which appends the worlds it keeps to RL[(it + 1) & 1]. Grids are
+    // bounded by the last length the host read (lagged like the running count) plus the interior-point
+    // worlds that could have failed since. Worlds still in a phase when no interior-point world runs
+    // any more finish it after the loop (run_solver: run_resto), so does a restarted world's interior
+    // point (the next ipm_loop).
+    const bool inl = p->resto_inline;
+    int* RL[2] = {p->d_lists + 4 * p->Wmax, p->d_lists + 5 * p->Wmax};
+    const volatile int* flr = p->h_flags;
+    const int W0 = nrun;
+    int rlast = 0, nprev = nrun;
+    if (inl) HIPCK(hipMemsetAsync(d.cnt + 12, 0, sizeof(unsigned), p->stream));
+    auto resto_iter = [&](int it, int nb_ipm) {
+        if (!inl) return;
+        const int par = it & 1;
+        hipLaunchKernelGGL(resto_publish, dim3(1), dim3(1), 0, p->stream, d, par);
+        const int nb = std::min(W0, rlast + nprev + nb_ipm);
+        nprev = nb_ipm;
+        if (nb <= 0) return;
+        NlpDev dr = d;
+        dr.resto = 1;
+        dr.K = d.opt.max_ls;
+        dr.b_in_cs = 0;
+        dr.rflag = -1;
+        dr.wl = RL[par];
+        dr.lcount = d.cnt + 14 + par;
+        dr.rl_app = RL[1 - par];
+        hipLaunchKernelGGL(resto_rows_G, dim3(d.nblk, nb), dim3(ROW_THREADS), 0, p->stream, dr);
+        hipLaunchKernelGGL(resto_world_G, dim3(nb), dim3(64), 0, p->stream, dr);
+        hipLaunchKernelGGL(eval_trials_all, dim3(p->T, nb), dim3(EVAL_THREADS), 0, p->stream, dr);
+        hipLaunchKernelGGL(resto_rows_Vs, dim3(d.nblk, nb * dr.K), dim3(ROW_THREADS), 0, p->stream, dr);
+        hipLaunchKernelGGL(resto_world_Vs, dim3(nb), dim3(64), 0, p->stream, dr);
+        launch_eval(p, dim3(p->T, nb), dr, 5);
+    };
     // Launches cover the active worlds only (NlpDev::wl): every line-search round's ipm_world_C
     // compacts the worlds still running / still searching into the next lists and publishes the
     // counts in mapped host memory, read after the round's one host synchronisation. Inactive
@@ -768,6 +809,7 @@ static int ipm_loop(armour_planner* p, int nrun) {
     int backtracked = nrun;
     for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
         const bool tl = it > 0 && p->spec && d.pcready && nrun <= p->tail_worlds;
+        d.rl_app = inl ? RL[it & 1] : nullptr;  // this iteration's failed line searches
         NlpDev di = d;
         di.wl = Li[cur];
         if (tl) di.lcount = d.cnt + 8 + (it & 1);
@@ -803,11 +845,13 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * ds.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs_all, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
+            resto_iter(it, nrun);
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
             if (tail) {
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
+                if (inl) rlast = flr[6 + ((it - 1) & 1)];
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;
@@ -843,6 +887,7 @@ static int ipm_loop(armour_planner* p, int nrun) {
                 nnext = ((volatile int*)p->h_flags)[0];
                 nsearch = ((volatile int*)p->h_flags)[1];
                 backtracked = nsearch;
+                if (inl && it > 0) rlast = flr[6 + ((it - 1) & 1)];
             }
         }
         if (tl) {
@@ -857,12 +902,14 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
+            resto_iter(it, nrun);
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
             if (tail) {
                 // iteration it - 1's running count: the worlds iteration it was launched for
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
+                if (inl) rlast = flr[6 + ((it - 1) & 1)];
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;  // iteration it had nothing to do
@@ -896,11 +943,13 @@ static int ipm_loop(armour_planner* p, int nrun) {
                 hipLaunchKernelGGL(ipm_world_C, dim3(nsearch), dim3(64), 0, p->stream, dc);
             }
         }
-        if (nnext == 0) break;  // every world converged, hit the cap, failed or left for restoration
+        resto_iter(it, nrun);
+        if (nnext == 0) break;  // every world converged, hit the cap, failed or is in a restoration phase
         HIPCK(hipGetLastError());
         cur = 1 - cur;
         nrun = nnext;
     }
+    d.rl_app = nullptr;
     HIPCK(hipGetLastError());
     return 0;
 }

@@ -116,11 +116,14 @@ def test_speculative_line_search_matches_sequential():
         assert np.array_equal(g_s[w], Q.constraints(w)) and np.array_equal(c_s[w], Q.link_centers(w))
 
 
-def test_restoration_one_round_matches_rounds():
+@pytest.mark.parametrize("variant", ["ARMOUR_RESTO_ROUNDS", "ARMOUR_RESTO_INLINE"])
+def test_restoration_one_round_matches_rounds(variant):
     """The restoration phase's one-round Armijo search (all max_ls trials' values at once, iterations
-    launched without a host synchronisation; planner.hip run_resto) gives bitwise the plans of the
-    phase's sequential rounds (ARMOUR_RESTO_ROUNDS), on full-range worlds a third of which end in
-    local infeasibility (status 4) and some of which restart the interior point"""
+    launched without a host synchronisation; planner.hip run_resto) and its iterations run inside the
+    interior-point loop (ipm_loop, the default) give bitwise the plans of the phase's sequential
+    rounds after the loop (ARMOUR_RESTO_ROUNDS) and of the one-round phases after the loop
+    (ARMOUR_RESTO_INLINE=0), on full-range worlds a third of which end in local infeasibility
+    (status 4) and some of which restart the interior point"""
     import os
 
     T, O = 40, 10
@@ -128,11 +131,11 @@ def test_restoration_one_round_matches_rounds():
     P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
     res_s, _ = P.plan(worlds)
     g_s = [P.constraints(w) for w in range(len(worlds))]
-    os.environ["ARMOUR_RESTO_ROUNDS"] = "1"
+    os.environ[variant] = "1" if variant == "ARMOUR_RESTO_ROUNDS" else "0"
     try:
         Q = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
     finally:
-        del os.environ["ARMOUR_RESTO_ROUNDS"]
+        del os.environ[variant]
     res_q, _ = Q.plan(worlds)
     assert sum(r["status"] == 4 for r in res_q) >= 8, "too few worlds in the restoration phase"
     for w, (a, b) in enumerate(zip(res_s, res_q)):
