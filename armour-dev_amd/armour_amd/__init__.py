@@ -65,6 +65,13 @@ class Timing(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class PlanOutput(ctypes.Structure):
+    """armour_plan_output (include/armour_hip.h): the single-world entry's result and the caller's
+    output arrays (null: skipped)"""
+    _fields_ = [("result", Result), ("timing", Timing), ("constraints", _dp), ("joint_bounds", _dp),
+                ("link_centers", _dp), ("link_generators", _dp), ("torque_radius", _dp)]
+
+
 def lib():
     global _LIB
     if _LIB is None:
@@ -92,6 +99,7 @@ def lib():
         L.armour_plan_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Result),
                                         ctypes.POINTER(Timing)]
         L.armour_reach_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(World), ctypes.POINTER(Timing)]
+        L.armour_plan.argtypes = [ctypes.c_void_p, ctypes.POINTER(World), ctypes.POINTER(PlanOutput)]
         L.armour_eval_constraints.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp, _dp, _dp]
         L.armour_get_reach_program.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.armour_get_monomial_counts.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
@@ -116,7 +124,7 @@ ABI_SYMBOLS = ["armour_copy_bandwidth", "armour_create", "armour_create_robot", 
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
                "armour_get_reach_dump", "armour_get_reach_occupancy", "armour_get_monomial_counts",
                "armour_create_armtd", "armour_plan_armtd_batch", "armour_reach_armtd_batch",
-               "armour_get_plane_cache_stats"]
+               "armour_get_plane_cache_stats", "armour_plan"]
 
 
 def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
@@ -195,6 +203,22 @@ class Planner:
         view["obstacles"] = np.where(counts > 0, block.ctypes.data + starts, 0)
         self.O = int(counts[0]) if n else 0
         return arr
+
+    def plan_one(self, world):
+        """armour_plan (the single-world entry): (result dict, timing dict, outputs dict) with the
+        payloads of the five .out files"""
+        arr = self._worlds([world])
+        m = self.num_constraints(np.asarray(world[4]).reshape(-1, 12).shape[0])
+        outs = dict(constraints=np.zeros(m), joint_bounds=np.zeros(28), link_centers=np.zeros((self.T, self.NJ, 3)),
+                    link_generators=np.zeros((self.T, self.NJ, 3, 6)), torque_radius=np.zeros((self.T, NF)))
+        po = PlanOutput()
+        for k, v in outs.items():
+            setattr(po, k, v.ctypes.data_as(_dp))
+        _check(lib().armour_plan(self.h, arr, ctypes.byref(po)))
+        r = po.result
+        res = dict(k_opt=np.array(r.k_opt[:]), feasible=bool(r.feasible), status=r.solver_status,
+                   iterations=r.iterations, evaluations=r.evaluations, cost=r.cost, kkt=r.kkt_error, error=r.error)
+        return res, po.timing.as_dict(), outs
 
     def plan(self, worlds):
         arr = self._worlds(worlds)

@@ -98,14 +98,9 @@ struct Lib {
     decltype(&armour_create) create;
     decltype(&armour_destroy) destroy;
     decltype(&armour_last_error) last_error;
-    decltype(&armour_plan_batch) plan_batch;
+    decltype(&armour_plan) plan;
     decltype(&armour_num_joints) num_joints;
     decltype(&armour_num_constraints) num_constraints;
-    decltype(&armour_get_link_centers) link_centers;
-    decltype(&armour_get_link_generators) link_generators;
-    decltype(&armour_get_torque_radius) torque_radius;
-    decltype(&armour_get_constraints) constraints;
-    decltype(&armour_get_joint_bounds) joint_bounds;
 
     bool load(std::string& why) {
         const char* env = std::getenv("ARMOUR_LIB");
@@ -123,14 +118,9 @@ struct Lib {
         sym(create, "armour_create");
         sym(destroy, "armour_destroy");
         sym(last_error, "armour_last_error");
-        sym(plan_batch, "armour_plan_batch");
+        sym(plan, "armour_plan");
         sym(num_joints, "armour_num_joints");
         sym(num_constraints, "armour_num_constraints");
-        sym(link_centers, "armour_get_link_centers");
-        sym(link_generators, "armour_get_link_generators");
-        sym(torque_radius, "armour_get_torque_radius");
-        sym(constraints, "armour_get_constraints");
-        sym(joint_bounds, "armour_get_joint_bounds");
         if (!ok) why = "libarmour_hip.so lacks an armour_* symbol";
         return ok;
     }
@@ -202,24 +192,25 @@ int plan_dir(const Lib& L, armour_planner* served, const std::string& dir) {
     w.num_obstacles = O;
     w.obstacles = O > 0 ? obs.data() : nullptr;
 
-    armour_result r;
-    armour_timing tm;
-    if (L.plan_batch(p, 1, &w, &r, &tm) != 0) return fail_out(out1, L.last_error());
+    // one plan through the single-world entry (armour_plan): the result and the payloads of the
+    // five .out files
+    const int NJ = L.num_joints(p);
+    const int m = L.num_constraints(p, O);
+    std::vector<double> centers((size_t)T * NJ * 3), gens((size_t)T * NJ * 18), rad((size_t)T * NF), g(m), bounds(4 * NF);
+    armour_plan_output po{};
+    po.constraints = g.data();
+    po.joint_bounds = bounds.data();
+    po.link_centers = centers.data();
+    po.link_generators = gens.data();
+    po.torque_radius = rad.data();
+    if (L.plan(p, &w, &po) != 0) return fail_out(out1, L.last_error());
+    const armour_result& r = po.result;
+    const armour_timing& tm = po.timing;
     std::cout << "        HIP: reachable sets " << tm.reach_ms << " ms, solver " << tm.nlp_ms << " ms, "
               << (r.feasible ? "found a feasible solution" : "no feasible solution") << std::endl;
     // a reach set over the library's capacity is not planned: reported as no feasible solution
     // (-1, MATLAB keeps its braking trajectory), with the reason on stderr
     if (r.error) std::fprintf(stderr, "        armour_main: %s\n", L.last_error());
-
-    const int NJ = L.num_joints(p);
-    const int m = L.num_constraints(p, O);
-    std::vector<double> centers((size_t)T * NJ * 3), gens((size_t)T * NJ * 18), rad((size_t)T * NF), g(m), bounds(4 * NF);
-    int rc = L.link_centers(p, 0, centers.data());
-    rc = rc ? rc : L.link_generators(p, 0, gens.data());
-    rc = rc ? rc : L.torque_radius(p, 0, rad.data());
-    rc = rc ? rc : L.constraints(p, 0, g.data());
-    rc = rc ? rc : L.joint_bounds(p, bounds.data());
-    if (rc) return fail_out(out1, L.last_error());
 
     // the reference's writers are ofstreams at setprecision(10) / (6) (armour_main.cu:319-398),
     // i.e. printf's %.10g / %.6g; std::to_chars(general, precision) is specified as exactly that

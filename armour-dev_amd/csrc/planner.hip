@@ -1212,6 +1212,18 @@ void armour_destroy(armour_planner* p) {
     delete p;
 }
 
+int armour_plan(armour_planner* p, const armour_world* world, armour_plan_output* out) {
+    if (!p || !world || !out) return fail(ARMOUR_E_ARG, "null argument");
+    int rc = armour_plan_batch(p, 1, world, &out->result, &out->timing);
+    if (rc) return rc;
+    if (out->constraints && (rc = armour_get_constraints(p, 0, out->constraints))) return rc;
+    if (out->joint_bounds && (rc = armour_get_joint_bounds(p, out->joint_bounds))) return rc;
+    if (out->link_centers && (rc = armour_get_link_centers(p, 0, out->link_centers))) return rc;
+    if (out->link_generators && (rc = armour_get_link_generators(p, 0, out->link_generators))) return rc;
+    if (out->torque_radius && (rc = armour_get_torque_radius(p, 0, out->torque_radius))) return rc;
+    return 0;
+}
+
 int armour_num_constraints(const armour_planner* p, int O) { return p ? p->d.nt + p->T * p->NJ * O + NF * 4 : ARMOUR_E_ARG; }
 int armour_num_joints(const armour_planner* p) { return p ? p->NJ : ARMOUR_E_ARG; }
 

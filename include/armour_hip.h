@@ -132,6 +132,22 @@ int armour_num_constraints(const armour_planner* p, int num_obstacles);
 int armour_plan_batch(armour_planner* p, int num_worlds, const armour_world* worlds, armour_result* results,
                       armour_timing* timing);
 
+/* One plan, the whole of one armour_main.cu process (:37-398) on a planner handle: the single-world
+ * entry of SURVEY.md §8(b). Inputs are the content of armour.in (caller-owned); the result and timing
+ * are written into *out, and so is every output array the caller supplies (null: skipped) — the
+ * payloads of the five .out files. Equivalent to armour_plan_batch with one world followed by the
+ * getters (world 0). 0 or a negative ARMOUR_E_* code; thread-safe per handle like every entry. */
+typedef struct armour_plan_output {
+    armour_result result;       /* k_opt (armour.out unless infeasible), feasible, solver status ... */
+    armour_timing timing;
+    double* constraints;        /* [m] at the final iterate (armour_constraints.out, first m lines) */
+    double* joint_bounds;       /* [28] (armour_constraints.out, last 28 lines) */
+    double* link_centers;       /* [T][NJ][3] (armour_joint_position_center.out) */
+    double* link_generators;    /* [T][NJ][3][6] (armour_joint_position_radius.out) */
+    double* torque_radius;      /* [T][7] (armour_control_input_radius.out) */
+} armour_plan_output;
+int armour_plan(armour_planner* p, const armour_world* world, armour_plan_output* out);
+
 /* The ARMTD comparison planner (kinova_planner_realtime_armtd_comparison/, "ACMP/"): the content
  * of one armtd.in (ACMP/armtd_main.cu:37-102). Joint rotations come from offline JRS tables that the
  * caller slices (KSI/uarmtd_planner.m:260-318) instead of the Bernstein trajectory; the plan keeps

@@ -69,7 +69,7 @@ def test_executable_built():
     # the executable resolves the C ABI from libarmour_hip.so with dlopen (a served client never
     # maps the HIP runtime): it names the entry points it binds and links no HIP library
     strings = subprocess.run(["strings", exe], capture_output=True, text=True).stdout
-    for sym in ("armour_create", "armour_plan_batch", "armour_get_link_centers", "libarmour_hip.so"):
+    for sym in ("armour_create", "armour_plan", "armour_num_constraints", "libarmour_hip.so"):
         assert sym in strings, sym
     needed = subprocess.run(["readelf", "-d", exe], capture_output=True, text=True).stdout
     assert "amdhip" not in needed and "libarmour_hip" not in needed

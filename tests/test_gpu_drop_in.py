@@ -145,3 +145,20 @@ def test_served_mode_matches_in_process(tmp_path):
         server.terminate()
         server.wait(timeout=30)
     assert not (srv / "armour.sock").exists()
+
+
+def test_single_world_entry_matches_batch():
+    """armour_plan (SURVEY.md §8(b)'s single-world entry, which armour_main calls) gives the plan and
+    the five .out payloads of armour_plan_batch with one world and the getters, bitwise"""
+    import numpy as np
+
+    world = A.make_world(11, 20, profile="survey")
+    P = A.Planner(T=128, max_obstacles=20, max_worlds=1)
+    r1, _, outs = P.plan_one(world)
+    (r0,), _ = P.plan([world])
+    assert np.array_equal(r0["k_opt"], r1["k_opt"]) and r0["feasible"] == r1["feasible"]
+    assert (r0["status"], r0["iterations"], r0["evaluations"]) == (r1["status"], r1["iterations"], r1["evaluations"])
+    assert np.array_equal(outs["constraints"], P.constraints(0))
+    assert np.array_equal(outs["link_centers"].ravel(), P.link_centers(0).ravel())
+    assert np.array_equal(outs["torque_radius"].ravel(), P.torque_radius(0).ravel())
+    assert np.array_equal(outs["link_generators"].ravel(), P.link_generators(0).ravel())
