@@ -62,6 +62,9 @@ struct armour_planner {
     // reach program (ProgramBuilder::ops) on the device
     Op* d_prog = nullptr;
     int* d_slot_off = nullptr;
+    uint64_t* d_live = nullptr;   // [nops][2] ProgramBuilder::live_masks (the LDS-arena reach kernel)
+    bool lds_arena = true;        // batches of at most one job per CU on the LDS-arena kernel (ARMOUR_LDS_ARENA=0: off)
+    int last_lds_fallback = 0;    // the last reach ran again on the HBM arena (a job outgrew the LDS arena)
     JrsJoint* d_jrs = nullptr;
     int nops = 0, nslots = 0;
     unsigned long long* d_bytes = nullptr;
@@ -255,6 +258,10 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             return rc;
         HIPCK(hipMemcpy(p->d_prog, pb.ops.data(), sizeof(Op) * pb.ops.size(), hipMemcpyHostToDevice));
         HIPCK(hipMemcpy(p->d_slot_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
+        // live slots at each op, for the per-job engine's LDS arena (reach_kernel<256, true>)
+        const std::vector<uint64_t> live = pb.live_masks();
+        if ((rc = p->alloc(&p->d_live, live.size()))) return rc;
+        HIPCK(hipMemcpy(p->d_live, live.data(), sizeof(uint64_t) * live.size(), hipMemcpyHostToDevice));
         if (std::getenv("ARMOUR_PROFILE_OPS")) {
             // =3: no op profiling; [start, end] wall clock (100 MHz) of every bundle of the last launch
             // after the op tables (bundle-engine load balance)
@@ -302,6 +309,15 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     ra.slot_off = p->d_slot_off;
     ra.nslots = p->nslots;
     ra.bytes = p->d_bytes;
+    ra.live = p->d_live;
+    if (const char* e = std::getenv("ARMOUR_LDS_ARENA")) p->lds_arena = std::atoi(e) != 0;
+    // ARMOUR_LDS_ARENA_SCALE=k (tests): 1/k of the LDS arena, to exercise the HBM fallback
+    {
+        const char* e = std::getenv("ARMOUR_LDS_ARENA_SCALE");
+        const int k = e ? std::max(1, std::atoi(e)) : 1;
+        ra.lds_h = LDS_ARENA_H / k;
+        ra.lds_c = LDS_ARENA_C / k;
+    }
     // ARMOUR_PROFILE_OPS=1: per-op cycles/terms; =2: phase totals (each distorts the other)
     const char* pm = std::getenv("ARMOUR_PROFILE_OPS");
     ra.prof = (pm && std::atoi(pm) == 2) ? nullptr : p->d_prof;
@@ -606,6 +622,8 @@ static int run_reach(armour_planner* p) {
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
     p->lane_engine = !(p->has_job && jobs <= p->job_max);
+    const bool lds = !p->lane_engine && p->lds_arena && !p->job_narrow && jobs <= p->ncu && !ra.dump && !ra.phase && !ra.prof;
+    p->last_lds_fallback = 0;
     const long nj = jobs * NF;
     HIPCK(hipEventRecord(p->ev[3], rs));
     if (p->armtd)
@@ -628,8 +646,11 @@ static int run_reach(armour_planner* p) {
         const int lg = (int)(bundles < slots ? bundles : slots);
         launch_lane(shape, lg, rs, p->d_rp, la, p->ro);
     } else {
-        // a batch that fits the chip in one round at two jobs per CU takes the wide kernel
-        if (jobs <= (long)REACH_WIDE_PER_CU * p->ncu && !p->job_narrow)
+        // a batch of at most one job per CU takes the LDS-arena kernel, one that fits the chip in one
+        // round at two jobs per CU the wide kernel
+        if (lds)
+            hipLaunchKernelGGL((reach_kernel<REACH_WIDE_THREADS, true>), dim3((int)jobs), dim3(REACH_WIDE_THREADS), 0, rs, p->d_rp, ra, p->ro);
+        else if (jobs <= (long)REACH_WIDE_PER_CU * p->ncu && !p->job_narrow)
             hipLaunchKernelGGL(reach_kernel<REACH_WIDE_THREADS>, dim3(grid), dim3(REACH_WIDE_THREADS), 0, rs, p->d_rp, ra, p->ro);
         else
             hipLaunchKernelGGL(reach_kernel<REACH_THREADS>, dim3(grid), dim3(REACH_THREADS), 0, rs, p->d_rp, ra, p->ro);
@@ -642,6 +663,21 @@ static int run_reach(armour_planner* p) {
         return fail(ARMOUR_E_HIP, "reach kernel finished without publishing its counters (sequence number mismatch)");
     std::vector<int> err(p->W);
     for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
+    if (lds && std::any_of(err.begin(), err.end(), [](int e) { return (e & ERR_ARENA) != 0; })) {
+        // a job's live values outgrew the LDS arena: the batch again on the HBM arena (jrs_kernel
+        // zeroes the counters; the JRS scalars come out the same)
+        p->last_lds_fallback = 1;
+        ra.rc.seq = ++p->reach_seq;
+        hipLaunchKernelGGL(jrs_kernel, dim3((int)((jobs * NF + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
+                           p->qdd0, p->d_jrs, p->rc, p->ro.err);
+        hipLaunchKernelGGL(reach_kernel<REACH_WIDE_THREADS>, dim3(grid), dim3(REACH_WIDE_THREADS), 0, rs, p->d_rp, ra, p->ro);
+        HIPCK(hipGetLastError());
+        HIPCK(hipEventRecord(p->ev[4], rs));
+        HIPCK(hipEventSynchronize(p->ev[4]));
+        if (sum[RSUM_SEQ] != p->reach_seq)
+            return fail(ARMOUR_E_HIP, "reach kernel finished without publishing its counters (sequence number mismatch)");
+        for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
+    }
     for (int k = 0; k < 8; k++) p->h_occ[k] = (unsigned long long)sum[1 + k];
     {
         float ms = 0;

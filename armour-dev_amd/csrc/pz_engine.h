@@ -31,6 +31,10 @@
 #include "common.h"
 #include "wave.h"
 
+namespace armour {
+constexpr int MAX_SLOTS = 96;  // handle slots of a reach program (ProgramBuilder)
+}
+
 #define AI __host__ __device__ inline __attribute__((always_inline))
 #define UNR _Pragma("unroll")
 
@@ -67,6 +71,11 @@ struct Arena {
     long hcap, ccap;
     long hused, cused;
     double bytes;  // algorithmic monomial bytes read + written by the operators of this job
+    // LDS-resident arena (reach_kernel's single-round variant): compacted to the live values when
+    // an op may not fit (arena_ensure); live: per op, the slots live at its start
+    // (ProgramBuilder::live_masks). lds = 0: bump allocation only (HBM arena)
+    int lds;
+    const uint64_t* live;
 };
 
 struct Ctx {
@@ -540,6 +549,90 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
         h.coff = c0;
         h.cnt = K;
     }
+}
+
+// LDS arena: move the blocks of the values live at op pc (their handles' hashes and coefficient
+// rows; views share their parent's block) to the bottom of the arena in allocation order and
+// repoint the handles; every thread of the group, at an op boundary (no operand pointer is held).
+// Chunks of one element per thread: all reads of a chunk before a barrier, then the writes; a block
+// only moves down, so a chunk's writes never reach the next chunk's sources.
+AI void arena_compact(Ctx& x, int pc) {
+    Arena& A = *x.A;
+    const Grp& g = x.g;
+    long* tb = reinterpret_cast<long*>(x.stage);  // [6][MAX_SLOTS] block table (stage is free here)
+    long *boh = tb, *bhc = tb + MAX_SLOTS, *boc = tb + 2 * MAX_SLOTS, *bcc = tb + 3 * MAX_SLOTS;
+    long *bnh = tb + 4 * MAX_SLOTS, *bnc = tb + 5 * MAX_SLOTS;
+    int* own = x.kp;  // [MAX_SLOTS + 3] owner flags, then block count and totals (keys are free too)
+    const uint64_t l0 = A.live[2 * pc], l1 = A.live[2 * pc + 1];
+    auto live = [&](int q) { return ((q < 64 ? l0 >> q : l1 >> (q - 64)) & 1ull) && x.H[q].cnt > 0; };
+    g.sync();
+    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
+        bool o = live(q);
+        for (int r = 0; o && r < q; r++)
+            if (live(r) && x.H[r].hoff == x.H[q].hoff) o = false;
+        own[q] = o ? 1 : 0;
+    }
+    g.sync();
+    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
+        if (!own[q]) continue;
+        int rk = 0;
+        for (int r = 0; r < MAX_SLOTS; r++) rk += own[r] && x.H[r].hoff < x.H[q].hoff;
+        boh[rk] = x.H[q].hoff;
+        bhc[rk] = x.H[q].cnt;
+        boc[rk] = x.H[q].coff;
+        bcc[rk] = (long)x.H[q].cnt * x.H[q].stride;
+    }
+    g.sync();
+    if (g.tid == 0) {
+        int nb = 0;
+        for (int q = 0; q < MAX_SLOTS; q++) nb += own[q];
+        long th = 0, tc = 0;
+        for (int r = 0; r < nb; r++) { bnh[r] = th; bnc[r] = tc; th += bhc[r]; tc += bcc[r]; }
+        own[MAX_SLOTS] = nb;
+        A.hused = th;
+        A.cused = tc;
+    }
+    g.sync();
+    const int nb = own[MAX_SLOTS];
+    const long th = A.hused, tc = A.cused;
+    auto block_of = [&](const long* pre, long q) {  // the last block whose compacted start <= q
+        int lo = 0, hi = nb - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= q) lo = mid; else hi = mid - 1;
+        }
+        return lo;
+    };
+    for (long base = 0; base < th; base += g.n) {
+        const long q = base + g.tid;
+        uint64_t v = 0;
+        if (q < th) { const int r = block_of(bnh, q); v = A.h[boh[r] + (q - bnh[r])]; }
+        g.sync();
+        if (q < th) A.h[q] = v;
+        g.sync();
+    }
+    for (long base = 0; base < tc; base += g.n) {
+        const long q = base + g.tid;
+        double v = 0;
+        if (q < tc) { const int r = block_of(bnc, q); v = A.c[boc[r] + (q - bnc[r])]; }
+        g.sync();
+        if (q < tc) A.c[q] = v;
+        g.sync();
+    }
+    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
+        if (!live(q)) continue;
+        for (int r = 0; r < nb; r++)
+            if (boh[r] == x.H[q].hoff) { x.H[q].hoff = bnh[r]; x.H[q].coff = bnc[r]; break; }
+    }
+    g.sync();
+}
+// before op pc: compact the LDS arena when fewer than nh hashes / nc coefficient rows are free
+// (every thread; the caller has synchronised, so the decision is uniform)
+AI void arena_ensure(Ctx& x, int pc, long nh, long nc) {
+    const Arena& A = *x.A;
+    if (!A.lds) return;
+    if (A.hcap - A.hused >= nh && A.ccap - A.cused >= nc) return;
+    arena_compact(x, pc);
 }
 
 // output header finish (thread 0): pruned amount into both independent parts (PZsparse.cu:347-349)

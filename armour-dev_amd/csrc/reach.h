@@ -190,7 +190,6 @@ struct Op {
     double s;
 };
 
-constexpr int MAX_SLOTS = 96;
 
 // thread-0 bodies are inlined too: an out-of-line variant (stack arrays passed through a lambda
 // into a nested out-of-line call) was miscompiled for gfx950 — tools/dump_ops.py localised it to
@@ -498,9 +497,27 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
     const bool stamp = (prof || x.phase) && tid == 0;
     long long c_end = stamp ? clock64() : 0;
 #endif
+    int prev_sync = 1;
     for (int pc = 0; pc < nops; pc++) {
         const Op op = prog[pc];
         const int par = op.par > 1 ? op.par : 1;  // ops pc .. pc + par - 1 run as one group
+        if (x.A->lds) {
+            // LDS arena: room for the op's output (its term count bounds the monomials it keeps),
+            // compacting to the live values when short; at most half the arena is asked for, a
+            // larger output that does not fit flags ERR_ARENA (planner.hip reruns on the HBM arena)
+            if (!prev_sync) x.g.sync();
+            long nh = 0, nc = 0;
+            switch (op.code) {
+                case OP_MUL: case OP_ADD: case OP_STACK3: case OP_ADD1D: case OP_CROSS_PP:
+                    nh = op_terms(x, op); nc = 9 * nh; break;
+                case OP_CROSS_C: nh = op_terms(x, op); nc = 3 * nh; break;
+                case OP_MAKE1D: case OP_MAKEROT: case OP_MAKEBOX: case OP_CONST: case OP_TRANSPOSE:
+                    nh = 64L * par; nc = 576L * par; break;
+                default: break;
+            }
+            arena_ensure(x, pc, nh < x.A->hcap / 2 ? nh : x.A->hcap / 2, nc < x.A->ccap / 2 ? nc : x.A->ccap / 2);
+        }
+        prev_sync = op.sync;
 #if defined(__HIP_DEVICE_COMPILE__)
         long long c0 = 0;
         if (stamp) {
@@ -712,6 +729,28 @@ struct ProgramBuilder {
         }
     }
     void rel(std::initializer_list<int> l) { for (int s : l) rel(s); }
+    // Slots whose value is live at the start of each op (a backward pass over the tape; an op reads
+    // the slots among its a, b, c fields — fields that are constants for its code count as reads
+    // too, which only keeps more alive), two 64-bit words per op. The per-job engine's LDS arena
+    // compacts to exactly these values (pz_engine.h arena_compact).
+    std::vector<uint64_t> live_masks() const {
+        const int n = (int)ops.size();
+        std::vector<uint64_t> m(2 * (size_t)n, 0);
+        uint64_t l0 = 0, l1 = 0;
+        auto set = [&](int q) { if (q >= 0 && q < nslots) { if (q < 64) l0 |= 1ull << q; else l1 |= 1ull << (q - 64); } };
+        for (int pc = n - 1; pc >= 0; pc--) {
+            const Op& op = ops[pc];
+            if (op.o >= 0 && op.o < nslots) {
+                if (op.o < 64) l0 &= ~(1ull << op.o); else l1 &= ~(1ull << (op.o - 64));
+            }
+            set(op.a);
+            set(op.b);
+            set(op.c);
+            m[2 * pc] = l0;
+            m[2 * pc + 1] = l1;
+        }
+        return m;
+    }
     void emit(int code, int o = -1, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
         Op op;
         op.code = code; op.o = o; op.a = a; op.b = b; op.c = c; op.i = i; op.s = s; op.sync = 1; op.par = 0;

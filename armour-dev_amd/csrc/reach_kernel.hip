@@ -5,8 +5,12 @@
 // handle table and payload pool, the (hash, index) keys and the operand staging buffer.
 // Two widths of the same kernel: 128 threads, four workgroups (eight waves) per CU, for batches
 // up to JOB_ENGINE_JOBS; 256 threads, two per CU, for batches that fit the chip in one round
-// (<= 2 x CUs jobs: the drop-in's single plan), where a job's latency is the reach time and the
-// extra waves shorten the large operators' passes. Both at the VGPR budget of two waves per SIMD.
+// (<= 2 x CUs jobs), where a job's latency is the reach time and the extra waves shorten the large
+// operators' passes. Both at the VGPR budget of two waves per SIMD. A third form for batches of at
+// most one job per CU (the drop-in's single plan): 256 threads whose arena lives in LDS (the rest
+// of the CU's 160 KB), compacted to the live values between ops (pz_engine.h arena_compact), so no
+// operator round-trips HBM for its operands or output; a job whose live values outgrow it flags
+// ERR_ARENA and the batch runs again on the HBM arena (planner.hip run_reach).
 #include "reach.h"
 
 namespace armour {
@@ -27,6 +31,11 @@ constexpr int KEY_CAP_LDS = REACH_CFG_KEYS;
 constexpr int STAGE_DOUBLES = REACH_CFG_STAGE;
 constexpr int REACH_WG_PER_CU = REACH_CFG_WG_PER_CU;
 constexpr int POOL_DOUBLES = 1024;   // handle payloads (ProgramBuilder::slot_offsets)
+// the LDS arena of the one-job-per-CU form: with the 256-thread kernel's other LDS (~41 KB) it fills
+// the CU's 160 KB; the live values of a job peak near 35 KB (tests/emu: every job of the survey
+// sample fits this capacity bitwise, smaller ones flag ERR_ARENA)
+constexpr int LDS_ARENA_H = 2048;
+constexpr int LDS_ARENA_C = 13184;
 
 // The reach phase's counters: the algorithmic byte count, the capacity maxima occ[8] (arena
 // hashes, arena rows, operator terms, link / torque k-only monomials) and the per-world error
@@ -144,11 +153,16 @@ struct ReachArgs {
     int mode;                   // engine diagnostics (Ctx::mode)
     unsigned long long* phase;  // optional phase cycle totals [16] (null: off; exclusive with prof)
     double* dump;               // optional op-by-op state of job 0 (null: off)
+    const uint64_t* live;       // [nops][2] live slots at each op (ProgramBuilder::live_masks), LDS arena form
+    int lds_h, lds_c;           // the LDS arena's capacity in use (<= LDS_ARENA_H / _C; smaller for tests)
 };
 
-// 2 waves per SIMD: 256 registers per lane (VGPR + AGPR); NT threads per job
-template <int NT>
-__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(REACH_CFG_WAVES_PER_SIMD, REACH_CFG_WAVES_PER_SIMD))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
+// 2 waves per SIMD: 256 registers per lane (VGPR + AGPR); NT threads per job; LA: the LDS arena (one
+// workgroup per CU: one wave per SIMD, 512 registers, no spills)
+template <int NT, bool LA = false>
+__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(LA ? 1 : REACH_CFG_WAVES_PER_SIMD, LA ? 1 : REACH_CFG_WAVES_PER_SIMD))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
+    __shared__ uint64_t lah[LA ? LDS_ARENA_H : 1];
+    __shared__ double lac[LA ? LDS_ARENA_C : 1];
     __shared__ PZH H[MAX_SLOTS];
     __shared__ double pool[POOL_DOUBLES + 9];  // + 9: header reads of a full 3x3 past a small slot
     __shared__ uint64_t kh[KEY_CAP_LDS];
@@ -192,10 +206,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     for (long job = blockIdx.x; job < njobs; job += gridDim.x) {
         const int w = (int)(job / a.T), t = (int)(job % a.T);
         if (threadIdx.x == 0) {
-            arena.h = a.arena_h + (long)blockIdx.x * a.arena_cap;
-            arena.c = a.arena_c + (long)blockIdx.x * a.arena_cap * 3;
-            arena.hcap = a.arena_cap;
-            arena.ccap = a.arena_cap * 3;
+            if (LA) {
+                arena.h = lah;
+                arena.c = lac;
+                arena.hcap = a.lds_h;
+                arena.ccap = a.lds_c;
+                arena.lds = 1;
+                arena.live = a.live;
+            } else {
+                arena.h = a.arena_h + (long)blockIdx.x * a.arena_cap;
+                arena.c = a.arena_c + (long)blockIdx.x * a.arena_cap * 3;
+                arena.hcap = a.arena_cap;
+                arena.ccap = a.arena_cap * 3;
+                arena.lds = 0;
+                arena.live = nullptr;
+            }
             arena.hused = 0;
             arena.cused = 0;
             arena.bytes = 0;

@@ -11,6 +11,8 @@ using namespace armour;
 
 static double* g_dump = nullptr;
 static int g_unfused = 0;
+static long g_lds_h = 0, g_lds_c = 0;  // > 0: a compacting arena of this capacity (the device's LDS arena)
+extern "C" void emu_set_lds_arena(long hcap, long ccap) { g_lds_h = hcap; g_lds_c = ccap; }
 extern "C" void emu_set_dump(double* d) { g_dump = d; }
 extern "C" void emu_set_unfused(int u) { g_unfused = u; }
 extern "C" void emu_set_stats(int* st) { armour::g_op_stats = st; }
@@ -56,7 +58,14 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     std::vector<int> kp(kcap);
     double red[18];
     int iscan[2];
-    Arena A{ah.data(), ac.data(), cap, cap * 3, 0, 0, 0.0};
+    Arena A{ah.data(), ac.data(), cap, cap * 3, 0, 0, 0.0, 0, nullptr};
+    const std::vector<uint64_t> live = pb.live_masks();
+    if (g_lds_h > 0) {
+        A.hcap = g_lds_h;
+        A.ccap = g_lds_c;
+        A.lds = 1;
+        A.live = live.data();
+    }
     int err = 0;
     Ctx x;
     x.g = Grp{0, 1};
@@ -88,6 +97,7 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     double scratch[2 * NF];
     run_program(x, rp, pb.ops.data(), (int)pb.ops.size(), T, t, q0, qd0, qdd0, out, 0, jrs, scratch, nullptr, g_dump);
     *arena_used = A.hused;
+    if (g_lds_h > 0 && err) *arena_used = -1;
     if (arena_bytes) *arena_bytes = A.bytes;
     if (nops) *nops = (int)pb.ops.size();
     if (nslots) *nslots = pb.nslots;
