@@ -51,7 +51,7 @@ struct WorldState {
     int cur;           // eval slot holding the current point
     int status;        // 0 running, 1 converged, 2 max_iter, 3 line-search failure, 4 reach over capacity,
                        // 5 local infeasibility (the restoration phase stalled or failed), 6 in the
-                       // restoration phase (WS_RESTO)
+                       // restoration phase (WS_RESTO), 7 restarting after it (WS_RESTART)
     int searching;     // 1 while the line search of this iteration has not accepted
     int accepted_ok;   // last acceptance passed the filter (0: forced after max_ls trials)
     int ftype;
@@ -67,6 +67,10 @@ struct WorldState {
     double rphi;
 };
 constexpr int WS_RESTO = 6;
+// A world whose restoration phase reached a point within every bound waits for its slacks and
+// multipliers (ipm_rows_init) before it runs again: status 0 would let a phase run inside the
+// interior-point loop hand it back to lists that still name it (planner.hip ipm_loop)
+constexpr int WS_RESTART = 7;
 
 struct NlpDev {
     int W, T, NJ, O, m, R, nblk, chunk;

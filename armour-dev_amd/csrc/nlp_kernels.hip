@@ -2322,7 +2322,7 @@ __global__ __launch_bounds__(ROW_THREADS) void resto_rows_G(NlpDev d) {
 // a restoration phase that reached a point within every bound hands the world back to the
 // interior point: a fresh filter and BFGS matrix at the current mu (slacks: ipm_rows_init)
 __device__ inline void resto_restart(const NlpDev& d, WorldState& S) {
-    S.status = 0;
+    S.status = WS_RESTART;  // running again once run_solver has set its slacks (ipm_collect)
     for (int i = 0; i < NF * NF; i++) S.H[i] = (i % (NF + 1) == 0) ? 1.0 : 0.0;
     S.first_update = 1;
     S.nfilt = 0;
@@ -2588,13 +2588,17 @@ __global__ void resto_publish(NlpDev d, int par) {
 
 // the worlds of list `in` (n entries; null: worlds 0..n-1) with status `st`, into `out`; the count
 // into the mapped host flag `flag` (one block)
-__global__ __launch_bounds__(1024) void ipm_collect(NlpDev d, const int* in, int n, int st, int* out, int flag) {
+// (set >= 0: the collected worlds' new status)
+__global__ __launch_bounds__(1024) void ipm_collect(NlpDev d, const int* in, int n, int st, int* out, int flag, int set) {
     __shared__ unsigned c;
     if (threadIdx.x == 0) c = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int w = in ? in[i] : i;
-        if (d.ws[w].status == st) out[atomicAdd(&c, 1u)] = w;
+        if (d.ws[w].status == st) {
+            out[atomicAdd(&c, 1u)] = w;
+            if (set >= 0) d.ws[w].status = set;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) d.flags[flag] = (int)c;

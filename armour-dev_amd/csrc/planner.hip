@@ -1084,13 +1084,13 @@ static int run_solver(armour_planner* p) {
     // most resto_max phases per world, S.nresto).
     const volatile int* fl = p->h_flags;
     while (rc == 0 && d.opt.resto_max > 0) {
-        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, WS_RESTO, Lr, 0);
+        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, WS_RESTO, Lr, 0, -1);
         HIPCK(hipStreamSynchronize(p->stream));
         const int nr = fl[0];
         if (nr == 0) break;
         if ((rc = run_resto(p, Lr, nr))) break;
-        // the restarted worlds: after the loop only they can be running (the phase reorders its lists)
-        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, 0, Li0, 0);
+        // the restarted worlds (WS_RESTART), running again from here
+        hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, WS_RESTART, Li0, 0, 0);
         HIPCK(hipStreamSynchronize(p->stream));
         const int ni = fl[0];
         if (ni == 0) break;

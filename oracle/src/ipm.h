@@ -8,15 +8,17 @@
 //   rows r = 0..m-1 (constraints, bounds [L_r, U_r], |bound| >= 1e19 means infinite) plus the
 //   n box bounds; each finite side k has slack s_k > 0 and multiplier z_k > 0;
 //   1. residuals r_d = grad f - sum_k z_k a_k, r_p = c_k(x) - s_k, errors E_0 / E_mu (Ipopt-scaled)
-//   2. barrier update: monotone (default, mu_strategy 0):
-//      mu <- max(tol/10, min(kappa_mu*mu, mu^theta)) while E_mu <= kappa_eps*mu; or adaptive
-//      (option 1; Ipopt's mu_strategy "adaptive", KPR/Parameters.h:57): LOQO oracle
-//      mu = 0.1 min(0.05 (1 - xi) / xi, 2)^3 avg(s z) in free mode, with the kkt-error
-//      globalisation falling back to the monotone rule
+//   2. barrier update: adaptive (the default, mu_strategy 1; Ipopt's mu_strategy "adaptive",
+//      KPR/Parameters.h:57): LOQO oracle mu = 0.1 min(0.05 (1 - xi) / xi, 2)^3 avg(s z) in free
+//      mode, floor tol/10, mu on the 2^(j/8) grid, with the kkt-error globalisation falling back
+//      to the monotone rule; or monotone (option 0):
+//      mu <- max(tol/10, min(kappa_mu*mu, mu^theta)) while E_mu <= kappa_eps*mu
 //   3. Newton step on the reduced 7x7 system (H + sum_k sigma_k a_k a_k^T) dx = -grad f + sum_k a_k (mu/s_k - sigma_k r_p,k)
 //   4. ds, dz, fraction-to-boundary step sizes
-//   5. Ipopt's filter line search (no restoration phase) on theta = ||c(x) - s||_1 and the
-//      barrier objective phi = f - mu sum ln s, at most max_ls backtracking trials
+//   5. Ipopt's filter line search on theta = ||c(x) - s||_1 and the barrier objective
+//      phi = f - mu sum ln s, at most max_ls backtracking trials; when it fails, a restoration
+//      phase (Gauss-Newton on the violation with a box barrier, at most resto_max phases) that
+//      restarts the interior point from a feasible point or ends in local infeasibility (status 4)
 //   6. multiplier update with Ipopt's kappa_sigma safeguard; damped BFGS update of H
 #pragma once
 

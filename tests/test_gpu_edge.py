@@ -117,17 +117,25 @@ def test_speculative_line_search_matches_sequential():
 
 
 @pytest.mark.parametrize("variant", ["ARMOUR_RESTO_ROUNDS", "ARMOUR_RESTO_INLINE"])
-def test_restoration_one_round_matches_rounds(variant):
+@pytest.mark.parametrize("case", ["survey", "boundary"])
+def test_restoration_one_round_matches_rounds(variant, case):
     """The restoration phase's one-round Armijo search (all max_ls trials' values at once, iterations
     launched without a host synchronisation; planner.hip run_resto) and its iterations run inside the
     interior-point loop (ipm_loop, the default) give bitwise the plans of the phase's sequential
     rounds after the loop (ARMOUR_RESTO_ROUNDS) and of the one-round phases after the loop
-    (ARMOUR_RESTO_INLINE=0), on full-range worlds a third of which end in local infeasibility
-    (status 4) and some of which restart the interior point"""
+    (ARMOUR_RESTO_INLINE=0): on full-range worlds a third of which end in local infeasibility
+    (status 4), and on the small boundary set, two of whose converging worlds restart the interior
+    point at a phase's first iteration (their line search failed at a point within every bound)"""
     import os
 
-    T, O = 40, 10
-    worlds = [A.make_world(s, O, profile="survey") for s in range(64)]
+    if case == "survey":
+        T, O = 40, 10
+        worlds = [A.make_world(s, O, profile="survey") for s in range(64)]
+    else:
+        fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "boundary_small_T20_O6.npz")))
+        T, O = int(fx["T"]), fx["obstacles"].shape[1]
+        worlds = [(fx["q0"][w], fx["qd0"][w], fx["qdd0"][w], fx["q_des"][w], fx["obstacles"][w])
+                  for w in range(len(fx["kinds"]))]
     P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
     res_s, _ = P.plan(worlds)
     g_s = [P.constraints(w) for w in range(len(worlds))]
@@ -137,11 +145,11 @@ def test_restoration_one_round_matches_rounds(variant):
     finally:
         del os.environ[variant]
     res_q, _ = Q.plan(worlds)
-    assert sum(r["status"] == 4 for r in res_q) >= 8, "too few worlds in the restoration phase"
+    assert sum(r["status"] == 4 for r in res_q) >= (8 if case == "survey" else 3), "too few worlds in the restoration phase"
     for w, (a, b) in enumerate(zip(res_s, res_q)):
         assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"]
         assert (a["iterations"], a["evaluations"], a["status"], a["feasible"]) == \
-            (b["iterations"], b["evaluations"], b["status"], b["feasible"])
+            (b["iterations"], b["evaluations"], b["status"], b["feasible"]), w
         assert np.array_equal(g_s[w], Q.constraints(w))
 
 
