@@ -64,7 +64,8 @@ struct armour_planner {
     int* d_slot_off = nullptr;
     uint64_t* d_live = nullptr;   // [nops][2] ProgramBuilder::live_masks (the LDS-arena reach kernel)
     bool lds_arena = true;        // batches of at most one job per CU on the LDS-arena kernel (ARMOUR_LDS_ARENA=0: off)
-    int last_lds_fallback = 0;    // the last reach ran again on the HBM arena (a job outgrew the LDS arena)
+    int last_lds_fallback = 0;
+    bool lds_trace = false;       // ARMOUR_LDS_TRACE=1: report LDS-arena overflows on stderr (diagnostics)    // the last reach ran again on the HBM arena (a job outgrew the LDS arena)
     JrsJoint* d_jrs = nullptr;
     int nops = 0, nslots = 0;
     unsigned long long* d_bytes = nullptr;
@@ -311,6 +312,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     ra.bytes = p->d_bytes;
     ra.live = p->d_live;
     if (const char* e = std::getenv("ARMOUR_LDS_ARENA")) p->lds_arena = std::atoi(e) != 0;
+    if (const char* e = std::getenv("ARMOUR_LDS_TRACE")) p->lds_trace = std::atoi(e) != 0;
     // ARMOUR_LDS_ARENA_SCALE=k (tests): 1/k of the LDS arena, to exercise the HBM fallback
     {
         const char* e = std::getenv("ARMOUR_LDS_ARENA_SCALE");
@@ -622,7 +624,7 @@ static int run_reach(armour_planner* p) {
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
     p->lane_engine = !(p->has_job && jobs <= p->job_max);
-    const bool lds = !p->lane_engine && p->lds_arena && !p->job_narrow && jobs <= p->ncu && !ra.dump && !ra.phase && !ra.prof;
+    const bool lds = !p->lane_engine && p->lds_arena && !p->job_narrow && jobs <= p->ncu && !ra.dump;
     p->last_lds_fallback = 0;
     const long nj = jobs * NF;
     HIPCK(hipEventRecord(p->ev[3], rs));
@@ -667,6 +669,13 @@ static int run_reach(armour_planner* p) {
         // a job's live values outgrew the LDS arena: the batch again on the HBM arena (jrs_kernel
         // zeroes the counters; the JRS scalars come out the same)
         p->last_lds_fallback = 1;
+        if (p->lds_trace) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, p->ev[3], p->ev[4]);
+            int nw = 0;
+            for (int w = 0; w < p->W; w++) nw += (err[w] & ERR_ARENA) != 0;
+            std::fprintf(stderr, "armour: LDS arena overflow in %d of %d worlds (launch %.3f ms), HBM rerun\n", nw, p->W, ms);
+        }
         ra.rc.seq = ++p->reach_seq;
         hipLaunchKernelGGL(jrs_kernel, dim3((int)((jobs * NF + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
                            p->qdd0, p->d_jrs, p->rc, p->ro.err);

@@ -66,23 +66,27 @@ struct PZH {
 };
 
 struct Arena {
-    uint64_t* h;
-    double* c;
     long hcap, ccap;
     long hused, cused;
     double bytes;  // algorithmic monomial bytes read + written by the operators of this job
     // LDS-resident arena (reach_kernel's single-round variant): compacted to the live values when
-    // an op may not fit (arena_ensure); live: per op, the slots live at its start
-    // (ProgramBuilder::live_masks). lds = 0: bump allocation only (HBM arena)
+    // an op may not fit (arena_ensure, Ctx::live). lds = 0: bump allocation only (HBM arena)
     int lds;
-    const uint64_t* live;
+    int ncompact;   // compactions and coefficient rows moved (diagnostics)
+    long cmoved;
 };
 
 struct Ctx {
     Grp g;
     PZH* H;            // handle table (LDS)
     double* pool;      // handle payload pool (LDS)
-    Arena* A;          // bump arena state (LDS), storage in HBM
+    Arena* A;          // bump arena state (LDS)
+    // arena storage: HBM, or the LDS arrays of reach_kernel<NT, true>. Held here (registers), set
+    // from the kernel's own arrays, so the compiler sees their address space: LDS accesses compile
+    // to ds_read / ds_write, not flat instructions (which take the vector-memory path)
+    uint64_t* ah;
+    double* ac;
+    const uint64_t* live;  // LDS arena: per op, the slots live at its start (ProgramBuilder::live_masks)
     uint64_t* kh;      // ordered keys: hash        (LDS, cap_lds entries)
     uint32_t* ki;      // ordered keys: term index
     int* kp;           // keep flags / scan
@@ -134,7 +138,7 @@ AI double* abs_(const Ctx& x, const PZH& h) { return x.pool + h.off + 3 * (h.R *
 
 // read monomial k of handle h into a 9-block (entries >= nel(h) are zero)
 AI void read_mono(const Ctx& x, const PZH& h, int k, double* out) {
-    const double* base = x.A->c + h.coff + (long)k * h.stride;
+    const double* base = x.ac + h.coff + (long)k * h.stride;
     const int n = nel(h);
     UNR for (int e = 0; e < 9; e++) {
         double v = 0.0;
@@ -145,7 +149,7 @@ AI void read_mono(const Ctx& x, const PZH& h, int k, double* out) {
         out[e] = v;
     }
 }
-AI uint64_t mono_hash(const Ctx& x, const PZH& h, int k) { return x.A->h[h.hoff + k]; }
+AI uint64_t mono_hash(const Ctx& x, const PZH& h, int k) { return x.ah[h.hoff + k]; }
 
 // ---------------------------------------------------------------------------------------------
 // wave / block primitives
@@ -256,8 +260,8 @@ struct Src {
 
 AI Src src_of(const Ctx& x, const PZH& p) {
     Src s;
-    s.h = x.A->h + p.hoff;
-    s.c = x.A->c + p.coff;
+    s.h = x.ah + p.hoff;
+    s.c = x.ac + p.coff;
     s.cnt = p.cnt;
     s.n = nel(p);
     s.stride = p.stride;
@@ -464,10 +468,11 @@ struct Terms {
 };
 
 // copy the sources into LDS (hashes, then effective coefficient rows), if they fit; else the
-// hashes alone, if they fit (the key order's searches are chains of dependent hash loads, the
+// hashes alone, if they fit (HBM arena only) (the key order's searches are chains of dependent hash loads, the
 // group passes' coefficient loads are independent). Uniform decision; the caller's barrier
 // publishes the staged copy.
 AI void stage_sources(Ctx& x, Terms& T) {
+    if (x.A->lds) return;  // the LDS arena: the sources are in LDS already (views read in place)
     int need = 0, need_h = 0;
     UNR for (int s = 0; s < 3; s++) if (s < T.ns) { need += T.S[s].cnt * (1 + T.S[s].n); need_h += T.S[s].cnt; }
     if (need_h > x.stage_cap) return;
@@ -531,6 +536,20 @@ AI void bytes_add(const Ctx& x, double b) {
     x.A->bytes += b;
 #endif
 }
+AI void int_add(int* p, int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicAdd(p, v);
+#else
+    *p += v;
+#endif
+}
+AI void int_min(int* p, int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicMin(p, v);
+#else
+    *p = v < *p ? v : *p;
+#endif
+}
 AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
     h.stride = stride;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -554,75 +573,134 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
 // LDS arena: move the blocks of the values live at op pc (their handles' hashes and coefficient
 // rows; views share their parent's block) to the bottom of the arena in allocation order and
 // repoint the handles; every thread of the group, at an op boundary (no operand pointer is held).
-// Chunks of one element per thread: all reads of a chunk before a barrier, then the writes; a block
-// only moves down, so a chunk's writes never reach the next chunk's sources.
+// Bookkeeping in parallel over the MAX_SLOTS handles: a block's owner is its lowest live slot, its
+// rank the number of distinct live blocks below it (allocation order is arena order, and compaction
+// keeps it), its new offsets the sizes of the blocks ranked before it. Blocks below the first one
+// that moves stay where they are. Moves in chunks of four elements per thread: all reads of a chunk
+// before a barrier, then the writes; a block only moves down, so a chunk's writes never reach the
+// next chunk's sources.
 AI void arena_compact(Ctx& x, int pc) {
     Arena& A = *x.A;
     const Grp& g = x.g;
-    long* tb = reinterpret_cast<long*>(x.stage);  // [6][MAX_SLOTS] block table (stage is free here)
-    long *boh = tb, *bhc = tb + MAX_SLOTS, *boc = tb + 2 * MAX_SLOTS, *bcc = tb + 3 * MAX_SLOTS;
-    long *bnh = tb + 4 * MAX_SLOTS, *bnc = tb + 5 * MAX_SLOTS;
-    int* own = x.kp;  // [MAX_SLOTS + 3] owner flags, then block count and totals (keys are free too)
-    const uint64_t l0 = A.live[2 * pc], l1 = A.live[2 * pc + 1];
-    auto live = [&](int q) { return ((q < 64 ? l0 >> q : l1 >> (q - 64)) & 1ull) && x.H[q].cnt > 0; };
+    long* tb = reinterpret_cast<long*>(x.stage);  // slot and block tables (the stage is free here)
+    long *key = tb, *shc = tb + MAX_SLOTS, *scc = tb + 2 * MAX_SLOTS;  // per slot: block hoff (-1: none), sizes
+    long *boh = tb + 3 * MAX_SLOTS, *bhc = tb + 4 * MAX_SLOTS, *boc = tb + 5 * MAX_SLOTS;  // per rank
+    long *bcc = tb + 6 * MAX_SLOTS, *bnh = tb + 7 * MAX_SLOTS, *bnc = tb + 8 * MAX_SLOTS;
+    int* own = x.kp;                  // [MAX_SLOTS] owner flags (the keys are free too)
+    int* rank = x.kp + MAX_SLOTS;     // [MAX_SLOTS]
+    int* misc = x.kp + 2 * MAX_SLOTS; // block count, first block that moves
+    constexpr int B = 16;             // table reads per batch (independent loads in flight)
+    static_assert(MAX_SLOTS % B == 0, "slot batches");
+    const uint64_t l0 = x.live[2 * pc], l1 = x.live[2 * pc + 1];
     g.sync();
     for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        bool o = live(q);
-        for (int r = 0; o && r < q; r++)
-            if (live(r) && x.H[r].hoff == x.H[q].hoff) o = false;
+        const bool lv = ((q < 64 ? l0 >> q : l1 >> (q - 64)) & 1ull) && x.H[q].cnt > 0;
+        key[q] = lv ? x.H[q].hoff : -1;
+        shc[q] = x.H[q].cnt;
+        scc[q] = (long)x.H[q].cnt * x.H[q].stride;
+    }
+    if (g.tid == 0) { misc[0] = 0; misc[1] = MAX_SLOTS; }
+    g.sync();
+    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
+        const long kq = key[q];
+        bool o = kq >= 0;
+        for (int r0 = 0; r0 < MAX_SLOTS; r0 += B) {
+            long kr[B];
+            UNR for (int u = 0; u < B; u++) kr[u] = key[r0 + u];
+            UNR for (int u = 0; u < B; u++) o = o && !(r0 + u < q && kr[u] == kq);
+        }
         own[q] = o ? 1 : 0;
     }
     g.sync();
     for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        if (!own[q]) continue;
+        const long kq = key[q];
+        if (kq < 0) continue;
         int rk = 0;
-        for (int r = 0; r < MAX_SLOTS; r++) rk += own[r] && x.H[r].hoff < x.H[q].hoff;
-        boh[rk] = x.H[q].hoff;
-        bhc[rk] = x.H[q].cnt;
-        boc[rk] = x.H[q].coff;
-        bcc[rk] = (long)x.H[q].cnt * x.H[q].stride;
+        for (int r0 = 0; r0 < MAX_SLOTS; r0 += B) {
+            long kr[B];
+            int orr[B];
+            UNR for (int u = 0; u < B; u++) { kr[u] = key[r0 + u]; orr[u] = own[r0 + u]; }
+            UNR for (int u = 0; u < B; u++) rk += (orr[u] && kr[u] < kq) ? 1 : 0;
+        }
+        rank[q] = rk;
+        if (own[q]) {
+            boh[rk] = kq;
+            bhc[rk] = shc[q];
+            boc[rk] = x.H[q].coff;
+            bcc[rk] = scc[q];
+            int_add(&misc[0], 1);
+        }
     }
     g.sync();
-    if (g.tid == 0) {
-        int nb = 0;
-        for (int q = 0; q < MAX_SLOTS; q++) nb += own[q];
-        long th = 0, tc = 0;
-        for (int r = 0; r < nb; r++) { bnh[r] = th; bnc[r] = tc; th += bhc[r]; tc += bcc[r]; }
-        own[MAX_SLOTS] = nb;
-        A.hused = th;
-        A.cused = tc;
+    const int nb = misc[0];
+    for (int i = g.tid; i < (nb > 0 ? nb : 1); i += g.n) {
+        long sh = 0, sc = 0;
+        for (int r0 = 0; r0 < i; r0 += B) {
+            long hr[B], cr[B];
+            UNR for (int u = 0; u < B; u++) { const int r = min(r0 + u, MAX_SLOTS - 1); hr[u] = bhc[r]; cr[u] = bcc[r]; }
+            UNR for (int u = 0; u < B; u++) if (r0 + u < i) { sh += hr[u]; sc += cr[u]; }
+        }
+        if (nb == 0) {
+            A.hused = 0;
+            A.cused = 0;
+            continue;
+        }
+        bnh[i] = sh;
+        bnc[i] = sc;
+        if (sh != boh[i] || sc != boc[i]) int_min(&misc[1], i);
+        if (i == nb - 1) {
+            A.hused = sh + bhc[i];
+            A.cused = sc + bcc[i];
+            A.ncompact++;
+        }
     }
     g.sync();
-    const int nb = own[MAX_SLOTS];
+    const int first = misc[1];
     const long th = A.hused, tc = A.cused;
+    if (g.tid == 0 && first < nb) A.cmoved += tc - bnc[first];
     auto block_of = [&](const long* pre, long q) {  // the last block whose compacted start <= q
-        int lo = 0, hi = nb - 1;
+        int lo = first, hi = nb - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (pre[mid] <= q) lo = mid; else hi = mid - 1;
         }
         return lo;
     };
-    for (long base = 0; base < th; base += g.n) {
-        const long q = base + g.tid;
-        uint64_t v = 0;
-        if (q < th) { const int r = block_of(bnh, q); v = A.h[boh[r] + (q - bnh[r])]; }
-        g.sync();
-        if (q < th) A.h[q] = v;
-        g.sync();
-    }
-    for (long base = 0; base < tc; base += g.n) {
-        const long q = base + g.tid;
-        double v = 0;
-        if (q < tc) { const int r = block_of(bnc, q); v = A.c[boc[r] + (q - bnc[r])]; }
-        g.sync();
-        if (q < tc) A.c[q] = v;
-        g.sync();
+    constexpr int E = 4;
+    if (first < nb) {
+        for (long base = bnh[first]; base < th; base += (long)E * g.n) {
+            uint64_t v[E];
+            UNR for (int e = 0; e < E; e++) {
+                const long q = base + g.tid + (long)e * g.n;
+                v[e] = 0;
+                if (q < th) { const int r = block_of(bnh, q); v[e] = x.ah[boh[r] + (q - bnh[r])]; }
+            }
+            g.sync();
+            UNR for (int e = 0; e < E; e++) {
+                const long q = base + g.tid + (long)e * g.n;
+                if (q < th) x.ah[q] = v[e];
+            }
+            g.sync();
+        }
+        for (long base = bnc[first]; base < tc; base += (long)E * g.n) {
+            double v[E];
+            UNR for (int e = 0; e < E; e++) {
+                const long q = base + g.tid + (long)e * g.n;
+                v[e] = 0;
+                if (q < tc) { const int r = block_of(bnc, q); v[e] = x.ac[boc[r] + (q - bnc[r])]; }
+            }
+            g.sync();
+            UNR for (int e = 0; e < E; e++) {
+                const long q = base + g.tid + (long)e * g.n;
+                if (q < tc) x.ac[q] = v[e];
+            }
+            g.sync();
+        }
     }
     for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        if (!live(q)) continue;
-        for (int r = 0; r < nb; r++)
-            if (boh[r] == x.H[q].hoff) { x.H[q].hoff = bnh[r]; x.H[q].coff = bnc[r]; break; }
+        if (key[q] < 0) continue;
+        x.H[q].hoff = bnh[rank[q]];
+        x.H[q].coff = bnc[rank[q]];
     }
     g.sync();
 }
@@ -872,8 +950,8 @@ __device__ inline __attribute__((always_inline)) void simplify_small(Ctx& x, int
     coff = bcast0(coff);
     ok = __builtin_amdgcn_readlane(ok, 0);
     if (ok && keep) {
-        x.A->h[hoff + pos] = h;
-        double* dst = x.A->c + coff + (long)pos * n;
+        x.ah[hoff + pos] = h;
+        double* dst = x.ac + coff + (long)pos * n;
         UNR for (int e = 0; e < n; e++) dst[e] = out[e];
     }
     SPHASE(11)
@@ -985,8 +1063,8 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
         const bool keep = pol.group(acc, out, red);
         if (keep && ok) {
             const long pos = kp[q];
-            x.A->h[hoff + pos] = kh[q];
-            double* dst = x.A->c + coff + pos * n;
+            x.ah[hoff + pos] = kh[q];
+            double* dst = x.ac + coff + pos * n;
             UNR for (int e = 0; e < n; e++) dst[e] = out[e];
         }
     }
@@ -1090,8 +1168,8 @@ AI void cross_const(Ctx& x, int o, int a, const CrossC& C) {
         coff = bcast0(coff);
         ok = __builtin_amdgcn_readlane(ok, 0);
         if (ok && keep) {
-            x.A->h[hoff + pos] = S.h[lane];
-            double* dst = x.A->c + coff + (long)pos * 3;
+            x.ah[hoff + pos] = S.h[lane];
+            double* dst = x.ac + coff + (long)pos * 3;
             UNR for (int e = 0; e < 3; e++) dst[e] = out[e];
         }
         UNR for (int e = 0; e < 9; e++) red[e] = wsum(red[e]);
@@ -1125,8 +1203,8 @@ AI void cross_const(Ctx& x, int o, int a, const CrossC& C) {
             UNR for (int e = 0; e < 9; e++) dummy[e] = 0.0;
             cross_const_mono(C, m, x.thr, out, dummy);
             const long pos = kp[k];
-            x.A->h[hoff + pos] = S.h[k];
-            double* dst = x.A->c + coff + pos * 3;
+            x.ah[hoff + pos] = S.h[k];
+            double* dst = x.ac + coff + pos * 3;
             UNR for (int e = 0; e < 3; e++) dst[e] = out[e];
         }
     }

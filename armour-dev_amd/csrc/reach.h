@@ -245,8 +245,8 @@ T0FN void t0_make_raw(Ctx& x, int o, int R, int C, const double* center, int nc,
     if (hd.cnt == K)
         UNR for (int m = 0; m < M; m++)
             if (keep[m]) {
-                x.A->h[hd.hoff + pos[m]] = h[m];
-                UNR for (int e = 0; e < 9; e++) if (e < n) x.A->c[hd.coff + (long)pos[m] * n + e] = acc[m][e];
+                x.ah[hd.hoff + pos[m]] = h[m];
+                UNR for (int e = 0; e < 9; e++) if (e < n) x.ac[hd.coff + (long)pos[m] * n + e] = acc[m][e];
             }
 }
 
@@ -302,9 +302,9 @@ T0FN void t0_transpose(Ctx& x, int o, int a) {
         for (int k = 0; k < A.cnt; k++) {
             double m[9];
             read_mono(x, A, k, m);
-            x.A->h[h.hoff + k] = mono_hash(x, A, k);
+            x.ah[h.hoff + k] = mono_hash(x, A, k);
             for (int i = 0; i < A.R; i++)
-                for (int jj = 0; jj < A.C; jj++) x.A->c[h.coff + (long)k * n + jj + i * A.C] = m[i + jj * A.R];
+                for (int jj = 0; jj < A.C; jj++) x.ac[h.coff + (long)k * n + jj + i * A.C] = m[i + jj * A.R];
         }
     bytes_add(x, 2.0 * A.cnt * (8.0 + 8.0 * n));
 }
@@ -364,8 +364,8 @@ T0FN void t0_emit_link(Ctx& x, const ReachOut& out, long j, int a, int l) {
     int jg = 0, kk = 0;
     double rad[3] = {ind(x, h, 0)[0], ind(x, h, 0)[1], ind(x, h, 0)[2]};
     for (int k = 0; k < h.cnt; k++) {
-        const uint64_t hh = x.A->h[h.hoff + k];
-        const double* c = x.A->c + h.coff + (long)k * 3;
+        const uint64_t hh = x.ah[h.hoff + k];
+        const double* c = x.ac + h.coff + (long)k * 3;
         if (hh < HASH_K_ONLY) {
             if (kk < CAP_LM) {
                 out.link_hash[base * CAP_LM + kk] = (uint16_t)hh;
@@ -400,8 +400,8 @@ T0FN void t0_emit_torque(Ctx& x, const ReachOut& out, long j, int a, int i, doub
     double rad = ind(x, h, 0)[0];
     int kk = 0;
     for (int k = 0; k < h.cnt; k++) {
-        const uint64_t hh = x.A->h[h.hoff + k];
-        double c = x.A->c[h.coff + (long)k * h.stride + (h.comp >= 0 ? h.comp : 0)];
+        const uint64_t hh = x.ah[h.hoff + k];
+        double c = x.ac[h.coff + (long)k * h.stride + (h.comp >= 0 ? h.comp : 0)];
         if (h.scaled) c = h.scale * c;
         if (hh < HASH_K_ONLY) {
             if (kk < CAP_UM) {
@@ -507,10 +507,22 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
             // larger output that does not fit flags ERR_ARENA (planner.hip reruns on the HBM arena)
             if (!prev_sync) x.g.sync();
             long nh = 0, nc = 0;
+            // (rows per output monomial: the output's element count, from the operand shapes)
+            auto nel = [&](int q) { return x.H[q].R * x.H[q].C; };
             switch (op.code) {
-                case OP_MUL: case OP_ADD: case OP_STACK3: case OP_ADD1D: case OP_CROSS_PP:
-                    nh = op_terms(x, op); nc = 9 * nh; break;
-                case OP_CROSS_C: nh = op_terms(x, op); nc = 3 * nh; break;
+                case OP_MUL: {
+                    const int na = nel(op.a), nbe = nel(op.b);
+                    nh = op_terms(x, op);
+                    nc = nh * (na == 1 ? nbe : (nbe == 1 ? na : x.H[op.a].R * x.H[op.b].C));
+                    break;
+                }
+                case OP_ADD: case OP_ADD1D: {
+                    const int na = nel(op.a), nbe = nel(op.b);
+                    nh = op_terms(x, op);
+                    nc = nh * (na > nbe ? na : nbe);
+                    break;
+                }
+                case OP_STACK3: case OP_CROSS_PP: case OP_CROSS_C: nh = op_terms(x, op); nc = 3 * nh; break;
                 case OP_MAKE1D: case OP_MAKEROT: case OP_MAKEBOX: case OP_CONST: case OP_TRANSPOSE:
                     nh = 64L * par; nc = 576L * par; break;
                 default: break;
@@ -658,7 +670,7 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
         if (g_hash_sink)
             for (int mi = 0; mi < par; mi++) {
                 const int mo = prog[pc + mi].o;
-                if (mo >= 0) g_hash_sink(pc + mi, x.A->h + x.H[mo].hoff, x.H[mo].cnt);
+                if (mo >= 0) g_hash_sink(pc + mi, x.ah + x.H[mo].hoff, x.H[mo].cnt);
             }
 #endif
         if (dump) {

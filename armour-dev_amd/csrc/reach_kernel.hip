@@ -185,6 +185,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     x.H = H;
     x.pool = pool;
     x.A = &arena;
+    x.live = a.live;
+    if (LA) {
+        x.ah = lah;
+        x.ac = lac;
+    } else {
+        x.ah = a.arena_h + (long)blockIdx.x * a.arena_cap;
+        x.ac = a.arena_c + (long)blockIdx.x * a.arena_cap * 3;
+    }
     for (int k = threadIdx.x; k < a.nslots; k += blockDim.x) H[k].off = a.slot_off[k];
     x.kh = kh; x.ki = ki; x.kp = kp; x.cap_lds = KEY_CAP_LDS;
     x.gkh = a.gkh + (long)blockIdx.x * a.gcap;
@@ -207,22 +215,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         const int w = (int)(job / a.T), t = (int)(job % a.T);
         if (threadIdx.x == 0) {
             if (LA) {
-                arena.h = lah;
-                arena.c = lac;
                 arena.hcap = a.lds_h;
                 arena.ccap = a.lds_c;
                 arena.lds = 1;
-                arena.live = a.live;
             } else {
-                arena.h = a.arena_h + (long)blockIdx.x * a.arena_cap;
-                arena.c = a.arena_c + (long)blockIdx.x * a.arena_cap * 3;
                 arena.hcap = a.arena_cap;
                 arena.ccap = a.arena_cap * 3;
                 arena.lds = 0;
-                arena.live = nullptr;
             }
             arena.hused = 0;
             arena.cused = 0;
+            arena.ncompact = 0;
+            arena.cmoved = 0;
             arena.bytes = 0;
             err = 0;
         }

@@ -36,6 +36,13 @@ def set_lds_arena(hcap=0, ccap=0):
     lib().emu_set_lds_arena(ctypes.c_long(hcap), ctypes.c_long(ccap))
 
 
+def compactions():
+    """(compactions, coefficient rows moved) of the last reach_job on the compacting arena"""
+    out = (ctypes.c_long * 2)()
+    lib().emu_compactions(out)
+    return out[0], out[1]
+
+
 def reach_job(world, T, t, fused=True):
     """Outputs of job (world, t) as the kernel writes them (fused: the program's cross products
     as single ops, else composed from views / products / differences / stack)."""
