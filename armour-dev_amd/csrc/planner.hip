@@ -804,17 +804,28 @@ static int ipm_loop(armour_planner* p, int nrun) {
     // worlds that could have failed since. Worlds still in a phase when no interior-point world runs
     // any more finish it after the loop (run_solver: run_resto), so does a restarted world's interior
     // point (the next ipm_loop).
-    const bool inl = p->resto_inline;
+    // A loop over one world runs its phases after the loop: there is no other world's iteration to
+    // overlap them with, and the phase launches would cost every iteration of the drop-in's plan.
+    // In a synchronised iteration the host knows the bound exactly (the phase list it read plus the
+    // worlds still searching after round 0) and launches nothing when it is 0.
+    const bool inl = p->resto_inline && nrun > 1;
     int* RL[2] = {p->d_lists + 4 * p->Wmax, p->d_lists + 5 * p->Wmax};
-    const volatile int* flr = p->h_flags;
+    volatile int* flr = p->h_flags;
     const int W0 = nrun;
     int rlast = 0, nprev = nrun;
     if (inl) HIPCK(hipMemsetAsync(d.cnt + 12, 0, sizeof(unsigned), p->stream));
-    auto resto_iter = [&](int it, int nb_ipm) {
+    auto resto_iter = [&](int it, int nb_ipm, int exact = -1) {
         if (!inl) return;
         const int par = it & 1;
+        if (exact == 0) {
+            // nothing appended since the last publish (no phase survivors, no searching world):
+            // no launch; the host stands in for this iteration's published length
+            flr[6 + par] = 0;
+            nprev = 0;
+            return;
+        }
         hipLaunchKernelGGL(resto_publish, dim3(1), dim3(1), 0, p->stream, d, par);
-        const int nb = std::min(W0, rlast + nprev + nb_ipm);
+        const int nb = std::min(W0, exact > 0 ? exact : rlast + nprev + nb_ipm);
         nprev = nb_ipm;
         if (nb <= 0) return;
         NlpDev dr = d;
@@ -988,7 +999,9 @@ static int ipm_loop(armour_planner* p, int nrun) {
                 hipLaunchKernelGGL(ipm_world_C, dim3(nsearch), dim3(64), 0, p->stream, dc);
             }
         }
-        resto_iter(it, nrun);
+        // (the phase list's bound: the length the host read for the previous phase iteration, plus
+        // the worlds that searched past round 0 and so could have failed)
+        resto_iter(it, nsearch, rlast + nsearch);
         if (nnext == 0) break;  // every world converged, hit the cap, failed or is in a restoration phase
         HIPCK(hipGetLastError());
         cur = 1 - cur;
