@@ -2127,6 +2127,9 @@ __device__ inline void world_Cs_body(const NlpDev& d, WorldState& S, int i) {
         }
     }
     const uint64_t u = __builtin_bit_cast(uint64_t, s);
+    // the trials' objective values, one per lane in a single load round (a load per trial inside
+    // the loop below waited a memory latency per trial)
+    const uint64_t uf = __builtin_bit_cast(uint64_t, lane < d.K ? d.fs[(long)i * d.K + lane] : 0.0);
     int chosen = -1;
     const double mu = S.mu;
     for (int k = 0; k < d.K; k++) {
@@ -2134,9 +2137,11 @@ __device__ inline void world_Cs_body(const NlpDev& d, WorldState& S, int i) {
         const uint32_t hi0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 2 * k);
         const uint32_t lo1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 2 * k + 1);
         const uint32_t hi1 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 2 * k + 1);
+        const uint32_t lof = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)uf, k);
+        const uint32_t hif = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uf >> 32), k);
         const double logt = __builtin_bit_cast(double, ((uint64_t)hi0 << 32) | lo0);
         const double rpt = __builtin_bit_cast(double, ((uint64_t)hi1 << 32) | lo1);
-        const double ft = d.fs[(long)i * d.K + k];
+        const double ft = __builtin_bit_cast(double, ((uint64_t)hif << 32) | lof);
         // (the filter does not change while a search goes on: an acceptance ends it)
         const bool filt = filter_pass(S, rpt, ft - mu * logt);
         if (threadIdx.x == 0 && chosen == k - 1 && S.status == 0 && S.searching) {
@@ -2171,14 +2176,18 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_D(NlpDev d) {
     block_reduce_n(wn, kinds, lds, out);
 }
 
-// pass D's world step: BFGS update, accept the trial point; every lane of the wave calls it
+// pass D's world step: BFGS update, accept the trial point; every lane of the wave calls it. The
+// vectors and scalars are formed by every lane alike (the same arithmetic in the same order, so the
+// same values on every lane, at the cost of one lane), and lane l < 49 updates H's element l: the
+// update's 98 divisions run side by side instead of one after another on lane 0. Within the one
+// wave, every lane's reads of H precede the first write in program order.
 __device__ inline void world_D_body(const NlpDev& d, WorldState& S, int w) {
     if (S.status != 0) return;
     double wn[NF];
     const double init[NF] = {};
     const int op[NF] = {};
     world_partials_at(d.partial2 + (long)w * d.nblk * KA2, d.nblk, KA2, init, op, wn);
-    if (threadIdx.x != 0) return;
+    const int lane = threadIdx.x;
     const double* grad = d.grad + ((long)S.cur * d.W + w) * NF;
     const double* gradt = d.grad + ((long)(1 - S.cur) * d.W + w) * NF;
     double sv[NF], y[NF], Hs[NF], ss = 0, sy = 0;
@@ -2189,27 +2198,52 @@ __device__ inline void world_D_body(const NlpDev& d, WorldState& S, int w) {
         ss += sv[j] * sv[j];
     }
     for (int j = 0; j < NF; j++) sy += sv[j] * y[j];
-    if (S.first_update && sy > 0 && ss > 1e-20) {
+    double Hm[NF * NF];
+#pragma unroll
+    for (int e = 0; e < NF * NF; e++) Hm[e] = S.H[e];
+    const bool first = S.first_update && sy > 0 && ss > 1e-20;
+    if (first) {
         double yy = 0;
         for (int j = 0; j < NF; j++) yy += y[j] * y[j];
         const double sc = yy / sy;
-        for (int i = 0; i < NF * NF; i++) S.H[i] = (i % (NF + 1) == 0) ? sc : 0.0;
-        S.first_update = 0;
+#pragma unroll
+        for (int e = 0; e < NF * NF; e++) Hm[e] = (e % (NF + 1) == 0) ? sc : 0.0;
     }
     double sHs = 0;
+#pragma unroll
     for (int i = 0; i < NF; i++) {
         Hs[i] = 0;
-        for (int j = 0; j < NF; j++) Hs[i] += S.H[i * NF + j] * sv[j];
+#pragma unroll
+        for (int j = 0; j < NF; j++) Hs[i] += Hm[i * NF + j] * sv[j];
         sHs += sv[i] * Hs[i];
+    }
+    // this lane's element (row li, column lj) and its current value
+    const int le = lane < NF * NF ? lane : 0, li = le / NF, lj = le % NF;
+    double h = 0, Hsi = 0, Hsj = 0;
+#pragma unroll
+    for (int e = 0; e < NF * NF; e++) h = e == le ? Hm[e] : h;
+#pragma unroll
+    for (int q = 0; q < NF; q++) {
+        Hsi = q == li ? Hs[q] : Hsi;
+        Hsj = q == lj ? Hs[q] : Hsj;
     }
     if (ss > 1e-20 && sHs > 1e-20) {
         const double theta = (sy >= 0.2 * sHs) ? 1.0 : 0.8 * sHs / (sHs - sy);
         double rv[NF], sr = 0;
         for (int j = 0; j < NF; j++) { rv[j] = theta * y[j] + (1 - theta) * Hs[j]; sr += sv[j] * rv[j]; }
-        if (sr > 1e-20)
-            for (int i = 0; i < NF; i++)
-                for (int j = 0; j < NF; j++) S.H[i * NF + j] += -Hs[i] * Hs[j] / sHs + rv[i] * rv[j] / sr;
+        if (sr > 1e-20) {
+            double rvi = 0, rvj = 0;
+#pragma unroll
+            for (int q = 0; q < NF; q++) {
+                rvi = q == li ? rv[q] : rvi;
+                rvj = q == lj ? rv[q] : rvj;
+            }
+            h += -Hsi * Hsj / sHs + rvi * rvj / sr;
+        }
     }
+    if (lane < NF * NF) S.H[lane] = h;
+    if (lane != 0) return;
+    if (first) S.first_update = 0;
     for (int j = 0; j < NF; j++) S.x[j] = S.xt[j];
     S.cur = 1 - S.cur;
     S.nfail = S.accepted_ok ? 0 : S.nfail + 1;

@@ -63,7 +63,8 @@ struct armour_planner {
     Op* d_prog = nullptr;
     int* d_slot_off = nullptr;
     uint64_t* d_live = nullptr;   // [nops][2] ProgramBuilder::live_masks (the LDS-arena reach kernel)
-    bool lds_arena = true;        // batches of at most one job per CU on the LDS-arena kernel (ARMOUR_LDS_ARENA=0: off)
+    bool lds_arena = false;       // batches of at most one job per CU on the LDS-arena kernel (ARMOUR_LDS_ARENA=1; measured
+                                  // no faster than the HBM arena)
     int last_lds_fallback = 0;
     bool lds_trace = false;       // ARMOUR_LDS_TRACE=1: report LDS-arena overflows on stderr (diagnostics)    // the last reach ran again on the HBM arena (a job outgrew the LDS arena)
     JrsJoint* d_jrs = nullptr;

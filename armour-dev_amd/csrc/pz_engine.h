@@ -573,7 +573,7 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
 // LDS arena: move the blocks of the values live at op pc (their handles' hashes and coefficient
 // rows; views share their parent's block) to the bottom of the arena in allocation order and
 // repoint the handles; every thread of the group, at an op boundary (no operand pointer is held).
-// Bookkeeping in parallel over the MAX_SLOTS handles: a block's owner is its lowest live slot, its
+// Owners and ranks in parallel over the MAX_SLOTS handles: a block's owner is its lowest live slot, its
 // rank the number of distinct live blocks below it (allocation order is arena order, and compaction
 // keeps it), its new offsets the sizes of the blocks ranked before it. Blocks below the first one
 // that moves stay where they are. Moves in chunks of four elements per thread: all reads of a chunk
@@ -633,26 +633,21 @@ AI void arena_compact(Ctx& x, int pc) {
     }
     g.sync();
     const int nb = misc[0];
-    for (int i = g.tid; i < (nb > 0 ? nb : 1); i += g.n) {
-        long sh = 0, sc = 0;
-        for (int r0 = 0; r0 < i; r0 += B) {
-            long hr[B], cr[B];
-            UNR for (int u = 0; u < B; u++) { const int r = min(r0 + u, MAX_SLOTS - 1); hr[u] = bhc[r]; cr[u] = bcc[r]; }
-            UNR for (int u = 0; u < B; u++) if (r0 + u < i) { sh += hr[u]; sc += cr[u]; }
+    if (g.tid == 0) {
+        // one thread: the sizes are independent loads, so the loop streams them (a parallel prefix,
+        // each thread summing the ranks below its own, gave wrong offsets on gfx950 while the host
+        // build of the same code was right; not kept)
+        long th0 = 0, tc0 = 0;
+        for (int r = 0; r < nb; r++) {
+            bnh[r] = th0;
+            bnc[r] = tc0;
+            if ((th0 != boh[r] || tc0 != boc[r]) && r < misc[1]) misc[1] = r;
+            th0 += bhc[r];
+            tc0 += bcc[r];
         }
-        if (nb == 0) {
-            A.hused = 0;
-            A.cused = 0;
-            continue;
-        }
-        bnh[i] = sh;
-        bnc[i] = sc;
-        if (sh != boh[i] || sc != boc[i]) int_min(&misc[1], i);
-        if (i == nb - 1) {
-            A.hused = sh + bhc[i];
-            A.cused = sc + bcc[i];
-            A.ncompact++;
-        }
+        A.hused = th0;
+        A.cused = tc0;
+        A.ncompact++;
     }
     g.sync();
     const int first = misc[1];
@@ -705,11 +700,16 @@ AI void arena_compact(Ctx& x, int pc) {
     g.sync();
 }
 // before op pc: compact the LDS arena when fewer than nh hashes / nc coefficient rows are free
-// (every thread; the caller has synchronised, so the decision is uniform)
+// (every thread; the caller has synchronised, so every thread reads the same state)
+// The barrier after the reads: a thread-0 op allocates (moves hused) as soon as thread 0 passes
+// here, and a wave still reading the arena state would then decide differently (an unmatched
+// compaction barrier).
 AI void arena_ensure(Ctx& x, int pc, long nh, long nc) {
     const Arena& A = *x.A;
     if (!A.lds) return;
-    if (A.hcap - A.hused >= nh && A.ccap - A.cused >= nc) return;
+    const bool room = A.hcap - A.hused >= nh && A.ccap - A.cused >= nc;
+    x.g.sync();
+    if (room) return;
     arena_compact(x, pc);
 }
 

@@ -497,6 +497,15 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
     const bool stamp = (prof || x.phase) && tid == 0;
     long long c_end = stamp ? clock64() : 0;
 #endif
+    // every handle empty at the job's start: the LDS arena's compaction reads the handles its live
+    // masks name, and a slot named before its first definition (an operand field an op does not
+    // use counts as a read) must not carry what the previous kernel left in LDS
+    for (int k = x.g.tid; k < MAX_SLOTS; k += x.g.n) {
+        x.H[k].cnt = 0;
+        x.H[k].hoff = 0;
+        x.H[k].coff = 0;
+    }
+    x.g.sync();
     int prev_sync = 1;
     for (int pc = 0; pc < nops; pc++) {
         const Op op = prog[pc];

@@ -49,7 +49,14 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     const long cap = 1 << 22;
     std::vector<uint64_t> ah(cap);
     std::vector<double> ac(cap * 3);
-    std::vector<PZH> H(pb.nslots);
+    // handles as LDS leaves them (garbage): run_program must not depend on their contents
+    std::vector<PZH> H(MAX_SLOTS);
+    for (int k = 0; k < MAX_SLOTS; k++) {
+        H[k].cnt = 1000 + 37 * k;
+        H[k].hoff = 7 * k;
+        H[k].coff = 11 * k;
+        H[k].stride = 9;
+    }
     int pool_n = 0;
     const std::vector<int> off = pb.slot_offsets(&pool_n);
     std::vector<double> pool(pool_n + 9);

@@ -88,3 +88,26 @@ def test_bench_step_matches_oracle_world_by_world():
     kkt = np.array([r["kkt"] for r in res])
     st = np.array([r["status"] for r in res])
     assert np.all(kkt[st == 0] <= 1e-4)
+
+
+def test_single_world_plans_match_oracle():
+    """The drop-in's batch — one world per call — takes other paths than the bench step: the
+    per-job reach engine on its LDS arena (reach_kernel<256, true>), the sync-free tail from the
+    second iteration, and restoration phases after the interior-point loop. The first 48 headline
+    worlds planned one at a time against the same frozen oracle plans: every decision identical,
+    and the solver's path (iterations, k_opt within 1e-8 when converged or feasible) for all but
+    at most one of them."""
+    fx = load()
+    T, O = int(fx["T"]), int(fx["O"])
+    n = 48
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=1)
+    off = []
+    for i in range(n):
+        (r,), _ = P.plan([A.make_world(int(fx["seed"][i]), O, profile="survey")])
+        assert r["feasible"] == bool(fx["feasible"][i]) and r["status"] == fx["status"][i], \
+            (i, r["feasible"], r["status"], int(fx["status"][i]), r["iterations"], int(fx["iterations"][i]))
+        dk = float(np.abs(r["k_opt"] - fx["k_opt"][i]).max())
+        if r["iterations"] != fx["iterations"][i] or ((r["status"] == 0 or r["feasible"]) and dk > 1e-8):
+            off.append((i, r["iterations"], int(fx["iterations"][i]), dk))
+    print(f"single-world plans: {n - len(off)}/{n} on the oracle's path; off: {off}")
+    assert len(off) <= 1, off
