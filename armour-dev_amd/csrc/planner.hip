@@ -796,39 +796,34 @@ static int ipm_loop(armour_planner* p, int nrun) {
     int* Li[2] = {p->d_lists, p->d_lists + p->Wmax};                  // worlds of an iteration
     int* Ls[2] = {p->d_lists + 2 * p->Wmax, p->d_lists + 3 * p->Wmax};  // worlds of a line-search round
     const int ns = nside_count(p);
-    // Restoration phases inside the loop (with the speculative machinery): after each iteration's
-    // interior-point launches, one phase iteration (run_resto's one-round form) for the worlds whose
-    // line search failed so far and are still in their phase. Iteration it's failures (accept_trial)
-    // and the worlds phase iteration it - 1 kept are appended to RL[it & 1]; resto_publish hands its
-    // length to phase iteration it, which appends the worlds it keeps to RL[(it + 1) & 1]. Grids are
-    // bounded by the last length the host read (lagged like the running count) plus the interior-point
-    // worlds that could have failed since. Worlds still in a phase when no interior-point world runs
-    // any more finish it after the loop (run_solver: run_resto), so does a restarted world's interior
-    // point (the next ipm_loop).
+    // Restoration phases inside the loop (with the speculative machinery): after each synchronised
+    // iteration's interior-point launches, one phase iteration (run_resto's one-round form) for the
+    // worlds whose line search failed so far and are still in their phase. Iteration it's failures
+    // (accept_trial) and the worlds phase iteration it - 1 kept are appended to RL[it & 1];
+    // resto_publish hands its length to phase iteration it, which appends the worlds it keeps to
+    // RL[(it + 1) & 1]. The host knows the bound exactly (the list length it read for phase
+    // iteration it - 1, plus the worlds still searching after round 0) and launches nothing when it
+    // is 0. Worlds still in a phase when the loop ends or turns sync-free finish it after the loop
+    // (run_solver: run_resto), and so does a restarted world's interior point (the next ipm_loop).
     // A loop over one world runs its phases after the loop: there is no other world's iteration to
-    // overlap them with, and the phase launches would cost every iteration of the drop-in's plan.
-    // In a synchronised iteration the host knows the bound exactly (the phase list it read plus the
-    // worlds still searching after round 0) and launches nothing when it is 0.
+    // overlap them with.
     const bool inl = p->resto_inline && nrun > 1;
     int* RL[2] = {p->d_lists + 4 * p->Wmax, p->d_lists + 5 * p->Wmax};
     volatile int* flr = p->h_flags;
     const int W0 = nrun;
-    int rlast = 0, nprev = nrun;
+    int rlast = 0;
     if (inl) HIPCK(hipMemsetAsync(d.cnt + 12, 0, sizeof(unsigned), p->stream));
-    auto resto_iter = [&](int it, int nb_ipm, int exact = -1) {
+    auto resto_iter = [&](int it, int bound) {
         if (!inl) return;
         const int par = it & 1;
-        if (exact == 0) {
+        if (bound == 0) {
             // nothing appended since the last publish (no phase survivors, no searching world):
             // no launch; the host stands in for this iteration's published length
             flr[6 + par] = 0;
-            nprev = 0;
             return;
         }
         hipLaunchKernelGGL(resto_publish, dim3(1), dim3(1), 0, p->stream, d, par);
-        const int nb = std::min(W0, exact > 0 ? exact : rlast + nprev + nb_ipm);
-        nprev = nb_ipm;
-        if (nb <= 0) return;
+        const int nb = std::min(W0, bound);
         NlpDev dr = d;
         dr.resto = 1;
         dr.K = d.opt.max_ls;
@@ -866,7 +861,13 @@ static int ipm_loop(armour_planner* p, int nrun) {
     int backtracked = nrun;
     for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
         const bool tl = it > 0 && p->spec && d.pcready && nrun <= p->tail_worlds;
-        d.rl_app = inl ? RL[it & 1] : nullptr;  // this iteration's failed line searches
+        // this iteration's failed line searches: inline phases in synchronised iterations only
+        // (there the bound is exact and an idle iteration launches nothing; in the sync-free tail the
+        // phase launches ran every iteration, ~60 us each, while one to four worlds ran to the
+        // iteration cap: a 64-world share measured 186.6 against ~125 us per tail iteration). A
+        // world whose search fails in the tail, and a phase still running when the tail starts, end
+        // their phase after the loop (run_resto); the per-world arithmetic is the same either way.
+        d.rl_app = (inl && !tl) ? RL[it & 1] : nullptr;
         NlpDev di = d;
         di.wl = Li[cur];
         if (tl) di.lcount = d.cnt + 8 + (it & 1);
@@ -902,13 +903,11 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * ds.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs_all, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
-            resto_iter(it, nrun);
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
             if (tail) {
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
-                if (inl) rlast = flr[6 + ((it - 1) & 1)];
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;
@@ -959,14 +958,12 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
-            resto_iter(it, nrun);
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
             if (tail) {
                 // iteration it - 1's running count: the worlds iteration it was launched for
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
-                if (inl) rlast = flr[6 + ((it - 1) & 1)];
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;  // iteration it had nothing to do
@@ -1002,7 +999,7 @@ static int ipm_loop(armour_planner* p, int nrun) {
         }
         // (the phase list's bound: the length the host read for the previous phase iteration, plus
         // the worlds that searched past round 0 and so could have failed)
-        resto_iter(it, nsearch, rlast + nsearch);
+        resto_iter(it, rlast + nsearch);
         if (nnext == 0) break;  // every world converged, hit the cap, failed or is in a restoration phase
         HIPCK(hipGetLastError());
         cur = 1 - cur;
