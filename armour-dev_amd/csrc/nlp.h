@@ -148,9 +148,11 @@ struct NlpDev {
     int rflag;              // mapped host flag that resto_world_G's count goes to
     // restoration phases inside the interior-point loop (planner.hip ipm_loop): a world whose line
     // search fails is appended here (cnt[12]), and so is every world resto_world_Vs keeps in its
-    // phase; resto_publish hands the list's length to the next phase iteration (null: phases run
-    // after the loop, run_resto)
+    // phase; resto_publish moves the list into the next phase iteration's (null: phases run after
+    // the loop, run_resto). pend_flag: mapped host flag the round's last world kernel stores the
+    // list's length into (the host's view of pending phase work)
     int* rl_app;
+    int* pend_flag;
     // Certified plane cache (plane_cache_kernel). The 36 planes of a buffered
     // obstacle and their offsets d, delta do not depend on x; only A . c(x) does. For every
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in

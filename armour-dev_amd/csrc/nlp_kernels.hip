@@ -2021,6 +2021,7 @@ __global__ __launch_bounds__(64) void ipm_world_C(NlpDev d) {
         if (d.ls0 && d.bt_flag) *d.bt_flag = (int)nsearch;
         d.flags[1] = (int)nsearch;
         if (d.lcount_out) *d.lcount_out = nsearch;
+        if (d.pend_flag) *d.pend_flag = (int)atomicAdd(&d.cnt[12], 0u);
         d.cnt[0] = 0;
         d.cnt[1] = 0;
         d.cnt[2] = 0;
@@ -2106,6 +2107,7 @@ __global__ __launch_bounds__(64) void ipm_world_Cs_all(NlpDev d) {
         if (d.lrun_out) *d.lrun_out = nrun;
         if (d.nrun_flag) *d.nrun_flag = (int)nrun;
         if (d.bt_flag) *d.bt_flag = (int)nbt;
+        if (d.pend_flag) *d.pend_flag = (int)atomicAdd(&d.cnt[12], 0u);
         d.cnt[0] = 0;
         d.cnt[1] = 0;
         d.cnt[2] = 0;
@@ -2611,13 +2613,19 @@ __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
     }
 }
 
-// the phase list's length (the worlds appended since the last publish: failed line searches of the
-// loop's last iteration and the worlds resto_world_Vs kept) for the phase iteration about to run:
-// cnt[14 + par] (its launches' lcount) and the mapped flags[6 + par] (the host, for grid bounds)
-__global__ void resto_publish(NlpDev d, int par) {
-    const unsigned n = atomicExch(&d.cnt[12], 0u);
-    d.cnt[14 + par] = n;
-    d.flags[6 + par] = (int)n;
+// the phase list of the next phase iteration: the worlds appended since the last publish (failed
+// line searches, and the worlds the last phase iteration kept) moved from the append list `src` to
+// `dst`, its length into cnt[14] (the phase launches' lcount); the append list starts empty again
+__global__ __launch_bounds__(256) void resto_publish(NlpDev d, const int* src, int* dst) {
+    __shared__ unsigned n;
+    if (threadIdx.x == 0) n = atomicAdd(&d.cnt[12], 0u);
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        d.cnt[14] = n;
+        d.cnt[12] = 0;
+    }
 }
 
 // the worlds of list `in` (n entries; null: worlds 0..n-1) with status `st`, into `out`; the count

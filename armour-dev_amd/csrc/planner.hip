@@ -503,6 +503,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     }
     HIPCK(hipMemset(d.cnt, 0, 16 * sizeof(unsigned)));
     d.rl_app = nullptr;
+    d.pend_flag = nullptr;
     d.lcount = nullptr;
     d.b_in_cs = 0;
     d.bt_flag = nullptr;
@@ -796,42 +797,42 @@ static int ipm_loop(armour_planner* p, int nrun) {
     int* Li[2] = {p->d_lists, p->d_lists + p->Wmax};                  // worlds of an iteration
     int* Ls[2] = {p->d_lists + 2 * p->Wmax, p->d_lists + 3 * p->Wmax};  // worlds of a line-search round
     const int ns = nside_count(p);
-    // Restoration phases inside the loop (with the speculative machinery): after each synchronised
-    // iteration's interior-point launches, one phase iteration (run_resto's one-round form) for the
-    // worlds whose line search failed so far and are still in their phase. Iteration it's failures
-    // (accept_trial) and the worlds phase iteration it - 1 kept are appended to RL[it & 1];
-    // resto_publish hands its length to phase iteration it, which appends the worlds it keeps to
-    // RL[(it + 1) & 1]. The host knows the bound exactly (the list length it read for phase
-    // iteration it - 1, plus the worlds still searching after round 0) and launches nothing when it
-    // is 0. Worlds still in a phase when the loop ends or turns sync-free finish it after the loop
-    // (run_solver: run_resto), and so does a restarted world's interior point (the next ipm_loop).
-    // A loop over one world runs its phases after the loop: there is no other world's iteration to
-    // overlap them with.
+    // Restoration phases inside the loop (with the speculative machinery): after an iteration's
+    // interior-point launches, one phase iteration (run_resto's one-round form) for the worlds whose
+    // line search failed and are still in their phase. Failures (accept_trial) and the worlds a
+    // phase iteration keeps are appended to one list RL (cnt[12]); resto_publish moves it into the
+    // phase list PL of the next phase iteration, so an iteration may launch no phase work at all
+    // and the appends wait for the next one that does. The host decides from the list length the
+    // round's last world kernel stores (pend_flag): in a synchronised iteration exactly (the length
+    // after round 0, plus the worlds still searching, which alone can fail now); in the sync-free
+    // tail from the length two iterations back (the last one it has read), so a phase starts at
+    // most two iterations late and at most two idle phase iterations follow the last one. Worlds
+    // still in a phase when the loop ends finish it after the loop (run_solver: run_resto), and so
+    // does a restarted world's interior point (the next ipm_loop). A loop over one world runs its
+    // phases after the loop: there is no other world's iteration to overlap them with.
     const bool inl = p->resto_inline && nrun > 1;
-    int* RL[2] = {p->d_lists + 4 * p->Wmax, p->d_lists + 5 * p->Wmax};
+    int* RL = p->d_lists + 4 * p->Wmax;
+    int* PL = p->d_lists + 5 * p->Wmax;
     volatile int* flr = p->h_flags;
     const int W0 = nrun;
-    int rlast = 0;
+    int pend_known = 0;  // the latest list length the host has read
+    int ub = 0;          // an upper bound of the list's length now: the last phase grid, plus every
+                         // interior-point world launched since (each could have failed)
     if (inl) HIPCK(hipMemsetAsync(d.cnt + 12, 0, sizeof(unsigned), p->stream));
-    auto resto_iter = [&](int it, int bound) {
-        if (!inl) return;
-        const int par = it & 1;
-        if (bound == 0) {
-            // nothing appended since the last publish (no phase survivors, no searching world):
-            // no launch; the host stands in for this iteration's published length
-            flr[6 + par] = 0;
-            return;
-        }
-        hipLaunchKernelGGL(resto_publish, dim3(1), dim3(1), 0, p->stream, d, par);
+    auto resto_iter = [&](int bound) {
+        if (!inl || bound <= 0) return;
+        hipLaunchKernelGGL(resto_publish, dim3(1), dim3(256), 0, p->stream, d, (const int*)RL, PL);
         const int nb = std::min(W0, bound);
+        ub = nb;  // the phase keeps at most the worlds it took
         NlpDev dr = d;
         dr.resto = 1;
         dr.K = d.opt.max_ls;
         dr.b_in_cs = 0;
         dr.rflag = -1;
-        dr.wl = RL[par];
-        dr.lcount = d.cnt + 14 + par;
-        dr.rl_app = RL[1 - par];
+        dr.wl = PL;
+        dr.lcount = d.cnt + 14;
+        dr.rl_app = RL;
+        dr.pend_flag = nullptr;
         hipLaunchKernelGGL(resto_rows_G, dim3(d.nblk, nb), dim3(ROW_THREADS), 0, p->stream, dr);
         hipLaunchKernelGGL(resto_world_G, dim3(nb), dim3(64), 0, p->stream, dr);
         hipLaunchKernelGGL(eval_trials_all, dim3(p->T, nb), dim3(EVAL_THREADS), 0, p->stream, dr);
@@ -861,13 +862,9 @@ static int ipm_loop(armour_planner* p, int nrun) {
     int backtracked = nrun;
     for (int it = 0; it <= d.opt.max_iter && nrun > 0; it++) {
         const bool tl = it > 0 && p->spec && d.pcready && nrun <= p->tail_worlds;
-        // this iteration's failed line searches: inline phases in synchronised iterations only
-        // (there the bound is exact and an idle iteration launches nothing; in the sync-free tail the
-        // phase launches ran every iteration, ~60 us each, while one to four worlds ran to the
-        // iteration cap: a 64-world share measured 186.6 against ~125 us per tail iteration). A
-        // world whose search fails in the tail, and a phase still running when the tail starts, end
-        // their phase after the loop (run_resto); the per-world arithmetic is the same either way.
-        d.rl_app = (inl && !tl) ? RL[it & 1] : nullptr;
+        // this iteration's failed line searches, and the list length its last world kernel reports
+        d.rl_app = inl ? RL : nullptr;
+        d.pend_flag = inl ? d.flags + 6 + (it & 1) : nullptr;
         NlpDev di = d;
         di.wl = Li[cur];
         if (tl) di.lcount = d.cnt + 8 + (it & 1);
@@ -903,11 +900,14 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * ds.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs_all, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
+            ub = std::min(W0, ub + nrun);
+            resto_iter(pend_known > 0 ? ub : 0);
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
             if (tail) {
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
+                if (inl) pend_known = flr[6 + ((it - 1) & 1)];
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;
@@ -943,7 +943,7 @@ static int ipm_loop(armour_planner* p, int nrun) {
                 nnext = ((volatile int*)p->h_flags)[0];
                 nsearch = ((volatile int*)p->h_flags)[1];
                 backtracked = nsearch;
-                if (inl && it > 0) rlast = flr[6 + ((it - 1) & 1)];
+                if (inl) pend_known = flr[6 + (it & 1)];  // after round 0 (ipm_world_C's last block)
             }
         }
         if (tl) {
@@ -958,12 +958,15 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_rows_Cs, dim3(d.nblk, nrun * d.K), dim3(ROW_THREADS), 0, p->stream, ds);
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
+            ub = std::min(W0, ub + nrun);
+            resto_iter(pend_known > 0 ? ub : 0);
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
             if (tail) {
                 // iteration it - 1's running count: the worlds iteration it was launched for
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
+                if (inl) pend_known = flr[6 + ((it - 1) & 1)];
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;  // iteration it had nothing to do
@@ -997,15 +1000,17 @@ static int ipm_loop(armour_planner* p, int nrun) {
                 hipLaunchKernelGGL(ipm_world_C, dim3(nsearch), dim3(64), 0, p->stream, dc);
             }
         }
-        // (the phase list's bound: the length the host read for the previous phase iteration, plus
-        // the worlds that searched past round 0 and so could have failed)
-        resto_iter(it, rlast + nsearch);
+        // (the phase list's bound: its length after round 0, plus the worlds that searched past
+        // round 0 and so could have failed)
+        if (inl) ub = std::min(W0, pend_known + nsearch);
+        resto_iter(ub);
         if (nnext == 0) break;  // every world converged, hit the cap, failed or is in a restoration phase
         HIPCK(hipGetLastError());
         cur = 1 - cur;
         nrun = nnext;
     }
     d.rl_app = nullptr;
+    d.pend_flag = nullptr;
     HIPCK(hipGetLastError());
     return 0;
 }
