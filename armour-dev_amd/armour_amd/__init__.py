@@ -21,7 +21,7 @@ _LIB = None
 _dp = ctypes.POINTER(ctypes.c_double)
 
 
-ARMOUR_E_ARG, ARMOUR_E_HIP, ARMOUR_E_CAPACITY, ARMOUR_E_STATE = -1, -2, -3, -4  # include/armour_hip.h
+ARMOUR_E_ARG, ARMOUR_E_HIP, ARMOUR_E_CAPACITY, ARMOUR_E_STATE, ARMOUR_E_INTERNAL = -1, -2, -3, -4, -5  # include/armour_hip.h
 
 
 class ArmourError(RuntimeError):
@@ -375,4 +375,4 @@ class ArmtdPlanner(Planner):
         return lib().armour_reach_armtd_batch(*a)
 
 
-__all__ = ["ArmtdPlanner", "Planner", "ArmourError", "ARMOUR_E_CAPACITY", "copy_bandwidth", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]
+__all__ = ["ArmtdPlanner", "Planner", "ArmourError", "ARMOUR_E_CAPACITY", "ARMOUR_E_INTERNAL", "copy_bandwidth", "default_batch", "make_world", "example_world", "csv_world", "straight_line_waypoint", "KINOVA", "LIB_PATH", "ABI_SYMBOLS"]

@@ -35,8 +35,11 @@
 // scale) for the answer; a server that does not answer in time leaves -1 in armour.out and a
 // non-zero exit, as any failed replan.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <limits.h>
+#include <poll.h>
 #include <signal.h>
+#include <sys/file.h>
 #include <sys/time.h>
 #include <sys/socket.h>
 #include <sys/un.h>
@@ -152,13 +155,38 @@ struct Text {
     }
 };
 
+// Served outputs are written as <file>.part and renamed into place only while the client still
+// waits, under an flock on <dir>/armour.lock that a timed-out client also takes before it writes
+// its -1: a plan that finishes after its client gave up (or after the next client truncated
+// armour.out) is discarded, never mixed into a later replan's files.
+bool peer_waiting(int fd) {
+    pollfd pf{fd, POLLIN, 0};
+    if (poll(&pf, 1, 0) < 0 || (pf.revents & (POLLHUP | POLLERR | POLLNVAL))) return false;
+    if (pf.revents & POLLIN) {
+        char b;
+        return recv(fd, &b, 1, MSG_PEEK | MSG_DONTWAIT) > 0;  // 0: the client closed its end
+    }
+    return true;
+}
+struct DirLock {
+    int fd;
+    explicit DirLock(const std::string& dir) : fd(open((dir + "armour.lock").c_str(), O_CREAT | O_RDWR, 0644)) {
+        if (fd >= 0) (void)!flock(fd, LOCK_EX);
+    }
+    ~DirLock() {
+        if (fd >= 0) { (void)!flock(fd, LOCK_UN); close(fd); }
+    }
+};
+
 // One replan of the buffer directory `dir`: read armour.in, plan, write the five outputs. With
-// `served` a planner of the right horizon is given (capacity MAX_OBSTACLE_NUM); otherwise one is
-// created for this input and destroyed.
-int plan_dir(const Lib& L, armour_planner* served, const std::string& dir) {
+// `served` a planner of the right horizon is given (capacity MAX_OBSTACLE_NUM) and `client` is the
+// requesting socket (outputs committed only while it waits); otherwise a planner is created for
+// this input and destroyed.
+int plan_dir(const Lib& L, armour_planner* served, const std::string& dir, int client = -1) {
     const std::string in = dir + "armour.in", out1 = dir + "armour.out";
-    // a fresh armour.out on every run, as the reference (armour_main.cu:36-37)
-    { std::ofstream o(out1); }
+    // a fresh armour.out on every run, as the reference (armour_main.cu:36-37); a served request's
+    // client truncated it already (a server must not touch the file of a client that gave up)
+    if (client < 0) { std::ofstream o(out1); }
 
     double q0[NF], qd0[NF], qdd0[NF], qdes[NF];
     int O = 0;
@@ -215,34 +243,53 @@ int plan_dir(const Lib& L, armour_planner* served, const std::string& dir) {
     // the reference's writers are ofstreams at setprecision(10) / (6) (armour_main.cu:319-398),
     // i.e. printf's %.10g / %.6g; std::to_chars(general, precision) is specified as exactly that
     // conversion and is several times faster for the ~40k numbers a T = 128 plan writes
+    std::vector<std::string> parts;  // served: the .part files to commit
+    auto dst = [&](const std::string& name) {
+        if (client < 0) return dir + name;
+        parts.push_back(dir + name);
+        return dir + name + ".part";
+    };
     Text o;
     if (r.feasible)
         for (int i = 0; i < NF; i++) o.num(r.k_opt[i], 10).ch('\n');
     else
         o.str("-1\n");
     o.str(std::to_string((long)(tm.reach_ms + tm.nlp_ms)));
-    if (!o.save(out1)) return 1;
+    if (!o.save(dst("armour.out"))) return 1;
     for (int t = 0; t < T; t++)
         for (int j = 0; j < NJ; j++) {
             for (int l = 0; l < 3; l++) o.num(centers[((size_t)t * NJ + j) * 3 + l], 10).ch(' ');
             o.ch('\n');
         }
-    if (!o.save(dir + "armour_joint_position_center.out")) return 1;
+    if (!o.save(dst("armour_joint_position_center.out"))) return 1;
     for (int t = 0; t < T; t++)
         for (int j = 0; j < NJ; j++)
             for (int k = 0; k < 3; k++) {
                 for (int l = 0; l < 6; l++) o.num(gens[(((size_t)t * NJ + j) * 3 + k) * 6 + l], 10).ch(' ');
                 o.ch('\n');
             }
-    if (!o.save(dir + "armour_joint_position_radius.out")) return 1;
+    if (!o.save(dst("armour_joint_position_radius.out"))) return 1;
     for (int t = 0; t < T; t++) {
         for (int j = 0; j < NF; j++) o.num(rad[(size_t)t * NF + j], 10).ch(' ');
         o.ch('\n');
     }
-    if (!o.save(dir + "armour_control_input_radius.out")) return 1;
+    if (!o.save(dst("armour_control_input_radius.out"))) return 1;
     for (int i = 0; i < m; i++) o.num(g[i], 6).ch('\n');
     for (int i = 0; i < 4 * NF; i++) o.num(bounds[i], 6).ch('\n');
-    if (!o.save(dir + "armour_constraints.out")) return 1;
+    if (!o.save(dst("armour_constraints.out"))) return 1;
+    if (client >= 0) {
+        if (const char* e = std::getenv("ARMOUR_SERVE_DELAY_MS")) usleep((useconds_t)std::atol(e) * 1000);  // tests
+        DirLock lk(dir);
+        const bool keep = peer_waiting(client);
+        for (const auto& f : parts) {
+            const std::string tmp = f + ".part";
+            if (!keep || std::rename(tmp.c_str(), f.c_str()) != 0) std::remove(tmp.c_str());
+        }
+        if (!keep) {
+            std::fprintf(stderr, "armour_main --serve: client of %s gave up; plan discarded\n", dir.c_str());
+            return 1;
+        }
+    }
     return 0;
 }
 
@@ -258,7 +305,7 @@ bool fill_addr(sockaddr_un& a, const std::string& path) {
 // sorted, as "K=V" joined by ';': client and server must agree on them
 std::string plan_env() {
     static const char* plumbing[] = {"ARMOUR_BUFFER_DIR=", "ARMOUR_SERVE_SOCKET=", "ARMOUR_NO_SERVE=",
-                                     "ARMOUR_SERVE_TIMEOUT_MS=", "ARMOUR_LIB="};
+                                     "ARMOUR_SERVE_TIMEOUT_MS=", "ARMOUR_SERVE_DELAY_MS=", "ARMOUR_LIB="};
     std::vector<std::string> kv;
     for (char** e = environ; *e; e++) {
         const std::string v = *e;
@@ -301,7 +348,12 @@ int try_served(const std::string& dir) {
     const bool got = sent && read(fd, &rc, 1) == 1;
     close(fd);
     if (got && rc == SERVE_REFUSED) return -1;
-    if (!got) return fail_out(out1, "the planning server did not answer (ARMOUR_SERVE_TIMEOUT_MS)");
+    if (!got) {
+        // the socket is closed first, so a server that finishes later sees the client gone and
+        // discards its plan; the lock orders this -1 against a commit already under way
+        DirLock lk(std::string(real) + "/");
+        return fail_out(out1, "the planning server did not answer (ARMOUR_SERVE_TIMEOUT_MS)");
+    }
     return (int)rc;
 }
 
@@ -358,7 +410,9 @@ int serve(const Lib& L, const std::string& dir) {
             } else {
                 std::string d = line.substr(0, t1);
                 if (!d.empty() && d.back() != '/') d += '/';
-                rc = (unsigned char)plan_dir(L, p, d);
+                // a request whose client already gave up (it waited in the backlog behind a long
+                // plan) is not planned
+                rc = peer_waiting(c) ? (unsigned char)plan_dir(L, p, d, c) : 1;
                 if (rc == SERVE_REFUSED) rc = 1;
             }
         }

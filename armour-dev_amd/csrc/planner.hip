@@ -65,8 +65,8 @@ struct armour_planner {
     uint64_t* d_live = nullptr;   // [nops][2] ProgramBuilder::live_masks (the LDS-arena reach kernel)
     bool lds_arena = false;       // batches of at most one job per CU on the LDS-arena kernel (ARMOUR_LDS_ARENA=1; measured
                                   // no faster than the HBM arena)
-    int last_lds_fallback = 0;
-    bool lds_trace = false;       // ARMOUR_LDS_TRACE=1: report LDS-arena overflows on stderr (diagnostics)    // the last reach ran again on the HBM arena (a job outgrew the LDS arena)
+    int last_lds_fallback = 0;    // the last reach ran again on the HBM arena (a job outgrew the LDS arena)
+    bool lds_trace = false;       // ARMOUR_LDS_TRACE=1: report LDS-arena overflows on stderr (diagnostics)
     JrsJoint* d_jrs = nullptr;
     int nops = 0, nslots = 0;
     unsigned long long* d_bytes = nullptr;
@@ -1112,9 +1112,10 @@ static int run_solver(armour_planner* p) {
         hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, WS_RESTO, Lr, 0, -1);
         HIPCK(hipStreamSynchronize(p->stream));
         const int nr = fl[0];
-        if (nr == 0) break;
-        if ((rc = run_resto(p, Lr, nr))) break;
-        // the restarted worlds (WS_RESTART), running again from here
+        if (nr > 0 && (rc = run_resto(p, Lr, nr))) break;
+        // the restarted worlds (WS_RESTART), running again from here. Collected whether or not a
+        // phase ran just now: a phase that ran inside ipm_loop may have restarted a world while
+        // other worlds were still iterating, and the loop never takes such a world back itself.
         hipLaunchKernelGGL(ipm_collect, dim3(1), dim3(1024), 0, p->stream, d, (const int*)nullptr, W, WS_RESTART, Li0, 0, 0);
         HIPCK(hipStreamSynchronize(p->stream));
         const int ni = fl[0];
@@ -1388,6 +1389,9 @@ static int plan_uploaded(armour_planner* p, armour_result* results, armour_timin
         r.cost = p->h_f[S.cur * p->d.W + w] / p->rp.cost_scale;
         r.kkt_error = S.kkt;
         r.error = p->world_err[w];
+        // a world the solver left in a non-terminal state (running, in a restoration phase, or
+        // waiting to restart) is a solver fault, never a silent "not planned"
+        if (!r.error && (S.status == 0 || S.status == WS_RESTO || S.status == WS_RESTART)) r.error = ARMOUR_E_INTERNAL;
         if (r.error) {
             r.solver_status = 3;
             r.feasible = 0;

@@ -28,7 +28,9 @@ enum {
     ARMOUR_E_ARG = -1,       /* invalid argument (sizes, null pointers) */
     ARMOUR_E_HIP = -2,       /* HIP runtime error / no device */
     ARMOUR_E_CAPACITY = -3,  /* a reach-set job exceeded its arena / sort / output capacity */
-    ARMOUR_E_STATE = -4      /* query before a plan / reach call */
+    ARMOUR_E_STATE = -4,     /* query before a plan / reach call */
+    ARMOUR_E_INTERNAL = -5   /* per-world result only: the solver left this world in a non-terminal
+                                state (a solver fault; reported infeasible, not planned) */
 };
 
 typedef struct armour_planner armour_planner;
@@ -66,7 +68,8 @@ typedef struct armour_result {
     double kkt_error;
     int error;           /* 0, or ARMOUR_E_CAPACITY: this world's reach set exceeded a capacity even
                             after the retry with 4x buffers; it is reported infeasible and not planned,
-                            the other worlds of the batch are (armour_plan_batch still returns 0) */
+                            the other worlds of the batch are (armour_plan_batch still returns 0);
+                            or ARMOUR_E_INTERNAL (a solver fault, never expected) */
 } armour_result;
 
 /* timings of the last batch, device-side (hipEvents on the planner's stream), milliseconds */

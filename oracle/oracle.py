@@ -168,7 +168,7 @@ class OraclePlanner:
             raise RuntimeError("oracle plan failed")
         return dict(k_opt=k, feasible=bool(feas), g=g, reach_ms=stats[0], nlp_ms=stats[1],
                     iterations=int(stats[2]), evaluations=int(stats[3]), status=int(stats[4]),
-                    cost=stats[5], kkt=stats[6])
+                    cost=stats[5], kkt=stats[6], restart_iter=int(stats[7]))
 
 
 class OracleArmtd(OraclePlanner):

@@ -242,7 +242,8 @@ int oracle_pz(void* h, int kind, int idx, double* center, double* indep, unsigne
 }
 
 // full plan: reach + NLP + finalize. stats[0]=reach ms, [1]=nlp ms, [2]=iterations, [3]=evals,
-// [4]=solver status, [5]=objective/cost_scale, [6]=kkt error. Returns 1 feasible, 0 infeasible, -1 error.
+// [4]=solver status, [5]=objective/cost_scale, [6]=kkt error, [7]=iteration count at the last
+// restart after a restoration phase (-1: none). Returns 1 feasible, 0 infeasible, -1 error.
 int oracle_plan_mu(void* h, double* k_opt, double* g_out, double* stats, int max_iter, int mu_strategy);
 int oracle_plan(void* h, double* k_opt, double* g_out, double* stats, int max_iter) {
     return oracle_plan_mu(h, k_opt, g_out, stats, max_iter, 1);
@@ -290,6 +291,7 @@ int oracle_plan_ex(void* h, double* k_opt, double* g_out, double* stats, int max
         stats[4] = r.status;
         stats[5] = r.obj / P->prm.cost_scale;
         stats[6] = r.kkt_error;
+        stats[7] = r.restart_iter;
     }
     return feas ? 1 : 0;
 }

@@ -135,7 +135,7 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
     // 1e-11; below ~tol / 10 the reduced system's Sigma = z / s ~ z^2 / mu of the active rows makes
     // the 1e-4-tolerance solution reproducible to ~1e-5 only: DESIGN.md §5, tools/mu_sensitivity.py)
     const double mu_min = (opt.mu_study & 2) ? 1e-11 : opt.tol / 10;
-    IpmResult res{1, 0, 0, 0.0, 0.0};
+    IpmResult res{1, 0, 0, 0.0, 0.0, -1};
     double a[NMAX], at[NMAX];
     int it;
     int nresto = 0;
@@ -438,6 +438,7 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             if (rs == 4) { res.status = 4; break; }
             // every row within its bounds: the interior point restarts at x (slacks and multipliers
             // as at the start, at the current mu; a fresh filter and BFGS matrix)
+            res.restart_iter = it;
             init_slacks();
             for (int i = 0; i < n * n; i++) H[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
             first_update = true;

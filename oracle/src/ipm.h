@@ -62,6 +62,7 @@ struct IpmResult {
     int evaluations;
     double obj;
     double kkt_error;
+    int restart_iter;  // iteration count at the last restoration phase that ended in a restart (-1: none)
 };
 
 // evaluation callback: f, grad f (n), g (m), dense row-major Jacobian (m x n)

@@ -147,6 +147,44 @@ def test_served_mode_matches_in_process(tmp_path):
     assert not (srv / "armour.sock").exists()
 
 
+def test_served_late_plan_is_discarded(tmp_path):
+    """A client that times out (ARMOUR_SERVE_TIMEOUT_MS) writes -1 and exits non-zero; the server's
+    plan for it finishes later (ARMOUR_SERVE_DELAY_MS holds it back here) and must not land in the
+    buffer directory: the server commits its .part files only while the client still waits, under
+    the directory's lock. The next replan is served normally."""
+    import time
+
+    T = 20
+    srv = tmp_path / "srv"
+    srv.mkdir()
+    env = dict(os.environ, ARMOUR_NUM_TIME_STEPS=str(T))
+    server = subprocess.Popen([EXE, "--serve", str(srv)], env=dict(env, ARMOUR_SERVE_DELAY_MS="1500"),
+                              stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        for _ in range(600):
+            if (srv / "armour.sock").exists() or server.poll() is not None:
+                break
+            time.sleep(0.1)
+        assert server.poll() is None and (srv / "armour.sock").exists(), "server did not start"
+        write_input(str(srv), A.example_world())
+        r = subprocess.run([EXE, str(srv)], env=dict(env, ARMOUR_SERVE_TIMEOUT_MS="300"), capture_output=True,
+                           text=True, timeout=60)
+        assert r.returncode != 0 and "did not answer" in r.stderr
+        time.sleep(3.0)  # the server's plan has finished by now, and was discarded
+        assert open(srv / "armour.out").read().split() == ["-1"]
+        assert not any(p.name.endswith(".part") for p in srv.iterdir())
+        assert not (srv / "armour_constraints.out").exists()
+        # a client that waits long enough gets the plan
+        r = subprocess.run([EXE, str(srv)], env=dict(env, ARMOUR_SERVE_TIMEOUT_MS="20000"), capture_output=True,
+                           text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        assert len(open(srv / "armour.out").read().split()) in (2, 8)
+        assert (srv / "armour_constraints.out").exists()
+    finally:
+        server.terminate()
+        server.wait(timeout=30)
+
+
 def test_single_world_entry_matches_batch():
     """armour_plan (SURVEY.md §8(b)'s single-world entry, which armour_main calls) gives the plan and
     the five .out payloads of armour_plan_batch with one world and the getters, bitwise"""

@@ -153,6 +153,30 @@ def test_restoration_one_round_matches_rounds(variant, case):
         assert np.array_equal(g_s[w], Q.constraints(w))
 
 
+def test_inline_restart_after_other_worlds_finish():
+    """A world whose restoration phase restarts the interior point inside ipm_loop (status
+    WS_RESTART) while another world is still iterating, after which that other world converges and
+    no world is left in a phase: run_solver must still collect and run the restarted world
+    (it was left at status 7 and reported 'not planned'). Boundary worlds 1, 8 and 9 of
+    the small set restart at iterations 1, 4 and 1 on the oracle; world 4 converges at 24 without
+    a phase. Every result matches the oracle's plan and carries no error."""
+    import os
+
+    fx = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "boundary_small_T20_O6.npz")))
+    T, O = int(fx["T"]), fx["obstacles"].shape[1]
+    world = lambda w: (fx["q0"][w], fx["qd0"][w], fx["qdd0"][w], fx["q_des"][w], fx["obstacles"][w])
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=2)
+    for pair in ((9, 4), (1, 4), (8, 4), (4, 9)):
+        res, _ = P.plan([world(w) for w in pair])
+        for w, r in zip(pair, res):
+            ref = OraclePlanner(*world(w), T=T, threads=4)
+            ref.reach()
+            ro = ref.plan()
+            assert r["error"] == 0, (pair, w, r)
+            assert (r["status"], r["iterations"], r["feasible"]) == (ro["status"], ro["iterations"], ro["feasible"]), (pair, w)
+            assert np.abs(r["k_opt"] - ro["k_opt"]).max() < 1e-8, (pair, w)
+
+
 @pytest.mark.parametrize("search", ["adaptive", "one", "rounds"])
 @pytest.mark.parametrize("tail", ["1000", "16"])
 def test_sync_free_tail_matches_synchronised(tail, search):
