@@ -34,6 +34,17 @@ constexpr int RCH = 6;                    // reduction slots combined per round 
 #endif
 
 #define DI __device__ inline __attribute__((always_inline))
+// Explicit address spaces for the simplify round loop: a pointer the
+// compiler cannot prove to be LDS or global becomes a flat access, which counts in both vmcnt and
+// lgkmcnt, so every LDS index read of a round waited for all of the wave's outstanding HBM loads and
+// stores. Key and group-head reads are LDS-typed (ds_read, lgkmcnt only), coefficient rows
+// global-typed (global_load / global_store, vmcnt only).
+#define GAS __attribute__((address_space(1)))
+#define LAS __attribute__((address_space(3)))
+template <class T>
+DI GAS T* gas(T* p) { return (GAS T*)p; }
+template <class T>
+DI GAS const T* gas(const T* p) { return (GAS const T*)p; }
 
 // bundle handle (LDS): union structure + where the lane data lives
 struct LH {
@@ -67,6 +78,9 @@ struct LCtx {
     uint32_t* ki;
     int* kp;
     int* gp;
+    LAS uint64_t* lkh;     // the same LDS arrays, LDS-typed (the round loop's reads)
+    LAS uint32_t* lki;
+    LAS int* lgp;
     int cap_lds;
     uint64_t* gkh;
     uint32_t* gki;
@@ -93,6 +107,13 @@ struct LCtx {
     long job;              // this lane's job index (clamped into range)
     bool valid;            // lane's job exists (the last bundle may be partial)
 };
+
+// Instrumentation (per-op cycles, simplify phase and round stamps, bundle wall clock) is compiled in
+// only with -DLANE_PROF=1 (make lane_variant LW=4 LX=_prof EXTRA=-DLANE_PROF=1): its counters and
+// time stamps otherwise stay live across the round loop and cost registers the product build needs.
+#ifndef LANE_PROF
+#define LANE_PROF 0
+#endif
 
 DI void sync() { __syncthreads(); }
 // phase stamps (profiling): thread 0 adds the cycles since the last stamp to prof[2 * nops + k]
@@ -129,6 +150,8 @@ DI long opaque(long v) {
 DI double opaque(double v) { return __builtin_bit_cast(double, opaque(__builtin_bit_cast(long, v))); }
 template <class T>
 DI const T* opaque(const T* p) { return (const T*)(uintptr_t)opaque((long)(uintptr_t)p); }
+template <class T>
+DI GAS const T* opaque(GAS const T* p) { return (GAS const T*)(uintptr_t)opaque((long)(uintptr_t)p); }
 
 // per-lane header rows
 DI double& P(const LCtx& x, int row) { return x.pool[(long)row * LG + x.lane]; }
@@ -575,8 +598,8 @@ struct LPolCrossPP {
 
 // rows of a full (non-view) block of N elements, monomial k
 template <int N>
-DI void rows(const double* c, int k, double* out, int lane) {
-    const double* base = c + (long)k * N * LG + lane;
+DI void rows(GAS const double* c, int k, double* out, int lane) {
+    GAS const double* base = c + (long)k * N * LG + lane;
 #pragma unroll
     for (int e = 0; e < N; e++) out[e] = base[(long)e * LG];
 }
@@ -587,30 +610,29 @@ struct GMul {
     static constexpr int NO = NA == 1 ? NB : (NB == 1 ? NA : 3 * (NB / 3));
     static constexpr int NV = NO;
     static constexpr int U = (NA == 9 && NB == 9) ? LANE_U99 : (NA == 9 ? 3 : 4);  // groups per wave round
-    const double* ca;
-    const double* cb;
+    GAS const double* ca;   // arena rows of monomial 0
+    GAS const double* cb;
+    GAS const double* pa;   // header pool rows of the operands' centres ([e][LG], as a monomial block)
+    GAS const double* pb;
     int na, nb;
     uint32_t nbm;
-    double Ac[NA], Bc[NB];
     DI void ra(int k, double* a, int lane) const { rows<NA>(ca, k, a, lane); }
     DI void rb(int k, double* b, int lane) const { rows<NB>(cb, k, b, lane); }
-    // Branch-free (p is wave-uniform): both factors' rows are always loaded, from clamped monomial
-    // indices (a handle without monomials reads a safe row, gen_mul), and the centre is selected in
-    // for T1 / T2 terms. A load inside a branch makes the compiler wait for it where the branches
-    // meet, which serialised the memory latencies of a round's groups.
+    // Branch-free (p is wave-uniform): each factor is read from one wave-uniform row block, a
+    // monomial's in the arena or the operand's centre in the header pool (T1: a_i x B.c, T2:
+    // A.c x b_j), chosen by a scalar select of the block address. A load inside a branch makes the
+    // compiler wait for it where the branches meet, and centres held in registers across the round
+    // loop cost 2 (NA + NB) VGPRs.
     DI void factors(int p, double* a, double* b, int lane) const {
         const bool ta = p < na, tb = !ta && p < na + nb;
         const int q = p - na - nb;
         const int iq = nb == 1 ? q : (int)__umulhi((uint32_t)(q > 0 ? q : 0), nbm);
-        const int i = ta ? p : (tb ? 0 : iq);
-        const int j = tb ? p - na : (ta ? 0 : q - iq * nb);
-        double la[NA], lb[NB];
-        ra(i, la, lane);
-        rb(j, lb, lane);
-#pragma unroll
-        for (int e = 0; e < NA; e++) a[e] = tb ? Ac[e] : la[e];
-#pragma unroll
-        for (int e = 0; e < NB; e++) b[e] = ta ? Bc[e] : lb[e];
+        const int i = ta ? p : iq;
+        const int j = tb ? p - na : q - iq * nb;
+        GAS const double* ba = tb ? pa : ca + (long)(i > 0 ? i : 0) * NA * LG;
+        GAS const double* bb = ta ? pb : cb + (long)(j > 0 ? j : 0) * NB * LG;
+        rows<NA>(ba, 0, a, lane);
+        rows<NB>(bb, 0, b, lane);
     }
     DI void term(int p, double* v, int lane) const {
         double a[NA], b[NB];
@@ -636,13 +658,11 @@ DI GMul<NA, NB> gen_mul(const LCtx& x, const LH& A, const LH& B) {
     G.nb = ui(B.cnt);
     // an operand without monomials (a constant matrix) points at the arena's first rows, so the
     // branch-free factors() never reads past an allocation
-    G.ca = up(x.A->c) + (G.na > 0 ? bcast0(A.coff) : 0) * LG;
-    G.cb = up(x.A->c) + (G.nb > 0 ? bcast0(B.coff) : 0) * LG;
+    G.ca = gas(up(x.A->c)) + (G.na > 0 ? bcast0(A.coff) : 0) * LG;
+    G.cb = gas(up(x.A->c)) + (G.nb > 0 ? bcast0(B.coff) : 0) * LG;
+    G.pa = gas(up(x.pool)) + (long)ui(A.off) * LG;
+    G.pb = gas(up(x.pool)) + (long)ui(B.off) * LG;
     G.nbm = G.nb > 1 ? 0xFFFFFFFFu / (uint32_t)G.nb + 1u : 0u;
-#pragma unroll
-    for (int e = 0; e < NA; e++) G.Ac[e] = cen(x, A, e);
-#pragma unroll
-    for (int e = 0; e < NB; e++) G.Bc[e] = cen(x, B, e);
     return G;
 }
 
@@ -667,7 +687,7 @@ struct GCat {
     static constexpr int U = N == 9 ? 2 : 4;
     // one descriptor per source, as plain scalars (an indexed member array would live in scratch)
     struct D {
-        const double* c;
+        GAS const double* c;
         int stride, comp, one, place, neg, scaled;
         double scale;
     };
@@ -680,7 +700,7 @@ struct GCat {
         // every term pays a chain of dependent scratch loads (descriptor, row, flags, scale).
         // (opaque(): the optimiser would fold a select of two field loads back into one load from
         // a selected address)
-        const double* c = s == 0 ? opaque(d0.c) : (s == 1 ? opaque(d1.c) : opaque(d2.c));
+        GAS const double* c = s == 0 ? opaque(d0.c) : (s == 1 ? opaque(d1.c) : opaque(d2.c));
         const int stride = s == 0 ? opaque(d0.stride) : (s == 1 ? opaque(d1.stride) : opaque(d2.stride));
         const int comp = s == 0 ? opaque(d0.comp) : (s == 1 ? opaque(d1.comp) : opaque(d2.comp));
         const int one = s == 0 ? opaque(d0.one) : (s == 1 ? opaque(d1.one) : opaque(d2.one));
@@ -689,7 +709,7 @@ struct GCat {
         const int scaled = s == 0 ? opaque(d0.scaled) : (s == 1 ? opaque(d1.scaled) : opaque(d2.scaled));
         const double scale = s == 0 ? opaque(d0.scale) : (s == 1 ? opaque(d1.scale) : opaque(d2.scale));
         const int k = s == 0 ? p : (s == 1 ? p - c0 : p - c0 - c1);
-        const double* base = c + (long)k * stride * LG + lane;
+        GAS const double* base = c + (long)k * stride * LG + lane;
         // branch-free: N loads either way (a 1x1 source reads its one element N times, the same
         // 512-byte row), then the same arithmetic as the per-element form
         const int e1 = comp >= 0 ? comp : 0;
@@ -708,7 +728,7 @@ struct GCat {
 template <int N>
 DI typename GCat<N>::D cat_desc(const LCtx& x, const LH& S, int neg, int place) {
     typename GCat<N>::D d;
-    d.c = up(x.A->c) + bcast0(S.coff) * LG;
+    d.c = gas(up(x.A->c)) + bcast0(S.coff) * LG;
     d.stride = ui(S.stride);
     d.comp = ui(S.comp);
     d.scaled = ui(S.scaled);
@@ -759,6 +779,30 @@ struct GAny {
 // lane = job: per-lane sums, decisions, pruned amounts; the group's keep mask is the ballot),
 // compaction scan over groups kept by any lane, pass 2 (copy), reduction, per-lane finish.
 // Sources staged and published by the caller's barrier. Ends with a barrier.
+// the end of the key window that starts at group g0 (operators beyond the LDS key capacity): the
+// most whole rounds of RG groups (or up to NG) whose keys and group heads fit the LDS arrays;
+// g0 itself when not even one round fits. Wave-uniform; gp is the global head array.
+DI int key_window_end(const LCtx& x, const int* gp, int g0, int NG, int RG) {
+    const int k0 = gp[g0];
+    const int nr = (NG - g0 + RG - 1) / RG;
+    // window of r rounds: groups [g0, min(g0 + r RG, NG)), fits when its groups and keys do
+    const int e1 = min(g0 + RG, NG);
+    if (e1 - g0 > x.cap_lds || gp[e1] - k0 > x.cap_lds) return g0;
+    int lo = 1, hi = nr;  // lo rounds fit; find the largest r <= nr that does (monotone)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        const int g1 = min(g0 + mid * RG, NG);
+        if (g1 - g0 <= x.cap_lds && gp[g1] - k0 <= x.cap_lds) lo = mid;
+        else hi = mid - 1;
+    }
+    return min(g0 + lo * RG, NG);
+}
+
+// ---- simplify over the union term list ----------------------------------------------------------
+// keys ordered by rank merge (once per bundle), group heads, pass 1 (each wave sums whole groups,
+// lane = job: per-lane sums, decisions, pruned amounts; the group's keep mask is the ballot),
+// compaction scan over groups kept by any lane, pass 2 (copy), reduction, per-lane finish.
+// Sources staged and published by the caller's barrier. Ends with a barrier.
 template <class Pol, class Gen>
 DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, int N) {
     constexpr int NV = Pol::NV, n = Pol::NO;
@@ -799,6 +843,10 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
     // round's kept prefix and writes its kept groups straight to their compacted rows. The output
     // reserves NG rows up front and gives back the unused tail at the end (no other allocation
     // runs during a simplify), so group values never leave registers.
+    // The rounds read keys and group heads from LDS only: an operator with more keys than the LDS
+    // arrays hold (sorted into the global buffers above) runs in windows of whole rounds, each
+    // window's keys and rebased heads copied into the LDS arrays first. Windows do not change which
+    // wave sums which group, or in what order, so the sums are those of one pass.
     constexpr int U = Gen::U;
     constexpr int RG = LW * U;
     static_assert(RG <= 64, "round masks fit one wave ballot");
@@ -811,11 +859,14 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
     LPHASE(3)
     const LH& ho = x.H[o];
     const bool ok = ui(ho.cnt) == NG;
-    double* dst = up(x.A->c) + bcast0(ho.coff) * LG + x.lane;
+    GAS double* const dst = gas(up(x.A->c)) + bcast0(ho.coff) * LG;  // wave-uniform; + lane at the store
     const long hoff = bcast0(ho.hoff);
-    uint64_t* const Ah = up(x.A->h);
-    uint64_t* const Am = up(x.A->m);
-    int base = 0;
+    GAS uint64_t* const Ah = gas(up(x.A->h));
+    GAS uint64_t* const Am = gas(up(x.A->m));
+    LAS const uint64_t* const lkh = x.lkh;
+    LAS const uint32_t* const lki = x.lki;
+    LAS int* const lgp = x.lgp;
+    int base = 0, par = 0;
     unsigned long long b = 0;
     unsigned long long sub[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long rt = x.prof ? clock64() : 0;
@@ -825,91 +876,113 @@ DI void simplify(LCtx& x, int o, const LTerms& T, const Gen& G, const Pol& pol, 
         sub[k] += (unsigned long long)(c_ - rt);                                                   \
         rt = c_;                                                                                   \
     }
-    for (int r0 = 0, par = 0; r0 < NG; r0 += RG, par ^= 1) {
-        RSTAMP(7)
-        // every index load of the round is issued before the first is used (clamped, no branches),
-        // then every group's first-member loads, so the round costs one latency per phase
-        int lo[U], sz[U];
-        int maxsz = 0;
-        {
-            int l0[U], h0[U];
+    for (int g0 = 0; g0 < NG;) {
+        int g1 = NG;
+        if (!in_lds) {
+            g1 = key_window_end(x, gp, g0, NG, RG);
+            if (g1 == g0) {  // not even one round's keys fit the LDS arrays
+                if (x.tid == 0) err_or(x, ERR_SORTCAP);
+                break;
+            }
+            const int k0 = gp[g0], k1 = gp[g1];
+            for (int q = x.tid; q < k1 - k0; q += LT) {
+                x.lki[q] = ki[k0 + q];
+                x.lkh[q] = kh[k0 + q];
+            }
+            for (int g = x.tid; g <= g1 - g0; g += LT) x.lgp[g] = gp[g0 + g] - k0;
+            sync();
+        }
+        const int ng = g1 - g0;  // groups of this window; lgp / lki / lkh indices are window-relative
+        for (int r0 = 0; r0 < ng; r0 += RG, par ^= 1) {
+            RSTAMP(7)
+            // every index load of the round is issued before the first is used (clamped, no
+            // branches), then every group's first-member loads, so the round costs one latency per phase
+            int lo[U], sz[U];
+            int maxsz = 0;
+            {
+                int l0[U], h0[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int g = min(r0 + x.wave * U + u, ng);
+                    l0[u] = lgp[g];
+                    h0[u] = lgp[min(g + 1, ng)];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const bool in = r0 + x.wave * U + u < ng;
+                    lo[u] = in ? ui(l0[u]) : 0;
+                    sz[u] = in ? ui(h0[u]) - lo[u] : 0;
+                    maxsz = sz[u] > maxsz ? sz[u] : maxsz;
+                }
+            }
+            RSTAMP(0)
+            if (LANE_PROF) {
+                sub[5] += 1;
+                sub[6] += maxsz;
+            }
+            double acc[U][NV];
+            uint64_t hk[U];  // the groups' hashes, loaded with the first members (stored after the barrier)
+            {
+                int p0[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    p0[u] = (int)lki[lo[u]];
+                    hk[u] = bcast0((long)lkh[lo[u]]);
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) G.term(ui(p0[u]), acc[u], x.lane);
+            }
+            for (int r = 1; r < maxsz; r++) {
+                double tmp[U][NV];
+                int pr[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) pr[u] = (int)lki[lo[u] + (r < sz[u] ? r : 0)];
+#pragma unroll
+                for (int u = 0; u < U; u++) G.term(ui(pr[u]), tmp[u], x.lane);
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (r < sz[u])
+#pragma unroll
+                        for (int e = 0; e < NV; e++) acc[u][e] = acc[u][e] + tmp[u][e];
+            }
+            double out[U][n];
+            unsigned long long mk[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const int g = min(r0 + x.wave * U + u, NG);
-                l0[u] = gp[g];
-                h0[u] = gp[min(g + 1, NG)];
+#pragma unroll
+                for (int e = 0; e < n; e++) out[u][e] = 0.0;
+                bool keep = false;
+                if (sz[u] > 0) keep = pol.group(acc[u], out[u], red);
+                mk[u] = ballot(keep);
+                if (x.lane == 0) x.rmask[par * 64 + x.wave * U + u] = mk[u];
             }
+            RSTAMP(1)
+            sync();
+            RSTAMP(2)
+            const unsigned long long km = ballot(x.lane < RG && r0 + x.lane < ng && x.rmask[par * 64 + x.lane] != 0);
 #pragma unroll
             for (int u = 0; u < U; u++) {
-                const bool in = r0 + x.wave * U + u < NG;
-                lo[u] = in ? ui(l0[u]) : 0;
-                sz[u] = in ? ui(h0[u]) - lo[u] : 0;
-                maxsz = sz[u] > maxsz ? sz[u] : maxsz;
+                if (mk[u] == 0 || !ok) continue;
+                const int idx = x.wave * U + u;
+                const long pos = base + __popcll(km & ((1ull << idx) - 1));
+#pragma unroll
+                for (int e = 0; e < n; e++) dst[(pos * n + e) * LG + x.lane] = out[u][e];
+                if (x.lane == 0) {
+                    Ah[hoff + pos] = hk[u];
+                    Am[hoff + pos] = mk[u];
+                }
+                b += (unsigned long long)__popcll(mk[u]) * (8ull + 8ull * n);  // wave-uniform
             }
+            base += __popcll(km);
+            RSTAMP(3)
         }
-        RSTAMP(0)
-        sub[5] += 1;
-        sub[6] += maxsz;
-        double acc[U][NV];
-        uint64_t hk[U];  // the groups' hashes, loaded with the first members (stored after the barrier)
-        {
-            int p0[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                p0[u] = (int)ki[lo[u]];
-                hk[u] = kh[lo[u]];
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) G.term(ui(p0[u]), acc[u], x.lane);
-        }
-        for (int r = 1; r < maxsz; r++) {
-            double tmp[U][NV];
-            int pr[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) pr[u] = (int)ki[lo[u] + (r < sz[u] ? r : 0)];
-#pragma unroll
-            for (int u = 0; u < U; u++) G.term(ui(pr[u]), tmp[u], x.lane);
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if (r < sz[u])
-#pragma unroll
-                    for (int e = 0; e < NV; e++) acc[u][e] = acc[u][e] + tmp[u][e];
-        }
-        double out[U][n];
-        unsigned long long mk[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-#pragma unroll
-            for (int e = 0; e < n; e++) out[u][e] = 0.0;
-            bool keep = false;
-            if (sz[u] > 0) keep = pol.group(acc[u], out[u], red);
-            mk[u] = ballot(keep);
-            if (x.lane == 0) x.rmask[par * 64 + x.wave * U + u] = mk[u];
-        }
-        RSTAMP(1)
-        sync();
-        RSTAMP(2)
-        const unsigned long long km = ballot(x.lane < RG && r0 + x.lane < NG && x.rmask[par * 64 + x.lane] != 0);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (mk[u] == 0 || !ok) continue;
-            const int idx = x.wave * U + u;
-            const long pos = base + __popcll(km & ((1ull << idx) - 1));
-#pragma unroll
-            for (int e = 0; e < n; e++) dst[(pos * n + e) * LG] = out[u][e];
-            if (x.lane == 0) {
-                Ah[hoff + pos] = hk[u];
-                Am[hoff + pos] = mk[u];
-                b += (unsigned long long)__popcll(mk[u]) * (8ull + 8ull * n);
-            }
-        }
-        base += __popcll(km);
-        RSTAMP(3)
+        g0 = g1;
+        if (!in_lds) sync();  // every wave is done with this window's keys before the next copy
     }
 #undef RSTAMP
     if (x.prof && x.tid == 0)
         for (int k = 0; k < 8; k++) atomicAdd(&x.prof[2 * x.nops + k], sub[k]);
-    if (b) atomicAdd(&x.A->bytes, b);
+    if (b && x.lane == 0) atomicAdd(&x.A->bytes, b);
     LPHASE(4)
     sync();
     if (x.tid == 0 && ok) {

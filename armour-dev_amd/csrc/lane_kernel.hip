@@ -82,6 +82,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     x.pool = a.pool + wg * a.pool_rows * LG;
     x.A = &arena;
     x.kh = kh; x.ki = ki; x.kp = kp; x.gp = gp; x.cap_lds = S::KEYS;
+    x.lkh = (LAS uint64_t*)(void*)kh;
+    x.lki = (LAS uint32_t*)(void*)ki;
+    x.lgp = (LAS int*)(void*)gp;
     x.gkh = a.gkh + wg * a.gcap;
     x.gki = a.gki + wg * a.gcap;
     x.gkp = a.gkp + wg * (a.gcap + 1);
@@ -99,7 +102,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     x.err = &err;
     x.occ = occ;
     x.thr = rp.simplify_threshold;
-    x.prof = a.prof;
+    x.prof = LANE_PROF ? a.prof : nullptr;
     x.nops = a.nops;
 
     // a retry (wlist) runs the listed worlds' jobs only, as consecutive bundles of their own
@@ -125,12 +128,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
         x.job = a.wlist ? (long)a.wlist[job / a.T] * a.T + job % a.T : job;
         x.jrs = a.jrs + x.job * NF;
         __syncthreads();
-        const unsigned long long t0 = a.btime ? wall_clock64() : 0;
+        unsigned long long* const btime = LANE_PROF ? a.btime : nullptr;
+        const unsigned long long t0 = btime ? wall_clock64() : 0;
         run_program(x, rp, a.prog, a.nops, out, b == 0 ? a.dump : nullptr);
         __syncthreads();
-        if (a.btime && x.tid == 0) {
-            a.btime[2 * b] = t0;
-            a.btime[2 * b + 1] = wall_clock64();
+        if (btime && x.tid == 0) {
+            btime[2 * b] = t0;
+            btime[2 * b + 1] = wall_clock64();
         }
         if (err && x.wave == 0 && x.valid) atomicOr(&out.err[x.job / a.T], err);
         if (x.tid == 0) {

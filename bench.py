@@ -53,10 +53,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=0,
                     help="worlds per planner per step (0: two whole bundle waves of the device, floor(2 * CUs * 64 / T): "
                          "327 on MI355X at T=100)")
-    ap.add_argument("--planners", type=int, default=3,
+    ap.add_argument("--planners", type=int, default=0,
                     help="planners per GPU planning their own batch concurrently (one HIP stream and one host thread "
-                         "each): one planner's solver fills the GPU around the others' (DESIGN.md section 6: 3 "
-                         "measured best, 2 about 2.5 %% behind, 4 behind)")
+                         "each): one planner's solver fills the GPU around the others'. 0 (default): 3 in weak mode "
+                         "(DESIGN.md section 6: measured best, 2 about 2.5 %% behind, 4 behind); in strong mode each "
+                         "rank times 1, 2 and 3 planners on its own share during warmup and keeps the fastest "
+                         "(DESIGN.md section 7: the best count depends on the share size)")
     ap.add_argument("--total-worlds", type=int, default=0,
                     help="strong scaling (config 4): one job of this many worlds sharded over the ranks")
     ap.add_argument("--T", type=int, default=100)
@@ -286,24 +288,38 @@ def main():
         geo = RT.geometry(robot)
         robot_name = "Fetch arm (URDF, 7 actuated + fixed gripper)"
 
-    P = a.planners
     strong = a.total_worlds > 0
+    auto_planners = strong and a.planners <= 0
+    if a.planners <= 0:
+        a.planners = 3
     if strong:
         mine = list(D.shard(a.total_worlds, rank, world_size))
-        per = -(-len(mine) // P)
-        subs_idx = [mine[p * per:(p + 1) * per] for p in range(P)]
-        subs_idx = [s for s in subs_idx if s]
-        P = len(subs_idx)
-        a.batch = max(len(s) for s in subs_idx)
+        worlds_mine = {i: A.make_world(i, a.O, robot=geo, profile=a.profile) for i in mine}
     else:
         if a.batch <= 0:
             a.batch = A.default_batch(a.T, local_rank)
-        mine = list(D.shard(a.batch * P * world_size, rank, world_size))
-        subs_idx = [mine[p * a.batch:(p + 1) * a.batch] for p in range(P)]
-    subs = [[A.make_world(i, a.O, robot=geo, profile=a.profile) for i in s] for s in subs_idx]
-    planners = [A.Planner(T=a.T, max_obstacles=a.O, max_worlds=len(s), device=local_rank, robot=robot) for s in subs]
-    n_rank = sum(len(s) for s in subs)
-    total_job = a.total_worlds if strong else a.batch * a.planners * world_size
+        mine = list(D.shard(a.batch * a.planners * world_size, rank, world_size))
+
+    def setup(nplan):
+        """this rank's worlds split over nplan planners: (sub-batches of world indices, worlds, planners)"""
+        if strong:
+            per = -(-len(mine) // nplan)
+            si = [mine[p * per:(p + 1) * per] for p in range(nplan)]
+            si = [x for x in si if x]
+            sw = [[worlds_mine[i] for i in x] for x in si]
+        else:
+            si = [mine[p * a.batch:(p + 1) * a.batch] for p in range(nplan)]
+            sw = [[A.make_world(i, a.O, robot=geo, profile=a.profile) for i in x] for x in si]
+        pl = [A.Planner(T=a.T, max_obstacles=a.O, max_worlds=len(x), device=local_rank, robot=robot) for x in sw]
+        return si, sw, pl
+
+    P = a.planners
+    subs_idx, subs, planners = setup(P)
+    P = len(planners)
+    if strong:
+        a.batch = max(len(x) for x in subs)
+    n_rank = sum(len(x) for x in subs)
+    total_job = a.total_worlds if strong else a.batch * P * world_size
 
     def fail(exc):
         print(f"bench: rank {rank}: {exc!r}", file=sys.stderr, flush=True)
@@ -314,6 +330,7 @@ def main():
     def plan_all():
         # one step: every planner plans its batch from its own host thread (ctypes releases the GIL
         # in armour_plan_batch); the collective below stays on this thread
+        P = len(planners)
         if P == 1:
             res, tm = planners[0].plan(subs[0])
             return res, [tm]
@@ -346,7 +363,36 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
+    calib = None
     try:
+        if auto_planners:
+            # strong mode: this rank's share is planned with 1, 2 and 3 concurrent planners (one
+            # untimed step, then the best of two timed steps each), and the fastest count is kept.
+            # Untimed for the bench line (warmup); the counts per share are in the line's config.
+            calib = {}
+            for cand in (1, 2, 3):
+                if cand > len(mine):
+                    continue
+                if cand != P:
+                    for pl in planners:
+                        pl.close()
+                    subs_idx, subs, planners = setup(cand)
+                    P = len(planners)
+                for pl, sw in zip(planners, subs):
+                    pl.plan(sw)
+                best_ms = float("inf")
+                for _ in range(2):
+                    t1 = time.perf_counter()
+                    plan_all()
+                    best_ms = min(best_ms, (time.perf_counter() - t1) * 1e3)
+                calib[str(cand)] = round(best_ms, 3)
+            keep = int(min(calib, key=calib.get))
+            if keep != P:
+                for pl in planners:
+                    pl.close()
+                subs_idx, subs, planners = setup(keep)
+                P = len(planners)
+            a.batch = max(len(x) for x in subs)
         for _ in range(a.warmup):
             # untimed: planners one after another, so first-launch costs do not pile up on one kernel
             res = [r for p in range(P) for r in planners[p].plan(subs[p])[0]]
@@ -397,6 +443,7 @@ def main():
                                   f"{P} concurrent planner(s) x {a.batch} worlds/GPU/step"),
                    "num_time_steps": a.T, "obstacles": a.O, "worlds_per_gpu": n_rank,
                    "planners_per_gpu": P, "worlds_per_planner": a.batch, "world_profile": a.profile,
+                   "planner_calibration_ms": calib,
                    "parallelism": f"world-sharded x{world_size}, RCCL all_gather of per-world records"},
         "breakdown_ms": {"reach": float(np.mean([t["reach_ms"] for t in tms])),
                          "nlp": float(np.mean([t["nlp_ms"] for t in tms])),
