@@ -29,8 +29,25 @@ constexpr int LG = 64;  // jobs per bundle = lanes per wave
 constexpr int LW = LANE_CFG_WAVES;        // waves per workgroup
 constexpr int LT = LW * LG;               // threads per workgroup
 constexpr int RCH = 6;                    // reduction slots combined per round across waves
+// groups per wave round of each generator (round width LW x U; lane_variant experiments; DESIGN.md
+// section 4 has the round-5 sweep: the defaults are the fastest measured)
 #ifndef LANE_U99
-#define LANE_U99 1                        // groups per wave round of a 3x3 x 3x3 product
+#define LANE_U99 1                        // 3x3 x 3x3 product
+#endif
+#ifndef LANE_U93
+#define LANE_U93 3                        // 3x3 x 3x1 product
+#endif
+#ifndef LANE_U13
+#define LANE_U13 4                        // 1x1 x 3x1 product
+#endif
+#ifndef LANE_UX
+#define LANE_UX 3                         // fused 3x1 x 3x1 cross product
+#endif
+#ifndef LANE_UC3
+#define LANE_UC3 4                        // concatenations of 1- / 3-element blocks
+#endif
+#ifndef LANE_UC9
+#define LANE_UC9 2                        // concatenations of 3x3 blocks
 #endif
 
 #define DI __device__ inline __attribute__((always_inline))
@@ -609,7 +626,7 @@ template <int NA, int NB>
 struct GMul {
     static constexpr int NO = NA == 1 ? NB : (NB == 1 ? NA : 3 * (NB / 3));
     static constexpr int NV = NO;
-    static constexpr int U = (NA == 9 && NB == 9) ? LANE_U99 : (NA == 9 ? 3 : 4);  // groups per wave round
+    static constexpr int U = (NA == 9 && NB == 9) ? LANE_U99 : (NA == 9 ? LANE_U93 : LANE_U13);  // groups per wave round
     GAS const double* ca;   // arena rows of monomial 0
     GAS const double* cb;
     GAS const double* pa;   // header pool rows of the operands' centres ([e][LG], as a monomial block)
@@ -669,7 +686,7 @@ DI GMul<NA, NB> gen_mul(const LCtx& x, const LH& A, const LH& B) {
 // fused PZ x PZ cross: the six 1x1 products of the term's factor rows (PolCrossPP)
 struct GCross {
     static constexpr int NV = 6;
-    static constexpr int U = 3;
+    static constexpr int U = LANE_UX;
     GMul<3, 3> M;  // factor rows only (3-element blocks both sides)
     DI void term(int p, double* v, int lane) const {
         double u[3], w[3];
@@ -684,7 +701,7 @@ struct GCross {
 template <int N>
 struct GCat {
     static constexpr int NV = N;
-    static constexpr int U = N == 9 ? 2 : 4;
+    static constexpr int U = N == 9 ? LANE_UC9 : LANE_UC3;
     // one descriptor per source, as plain scalars (an indexed member array would live in scratch)
     struct D {
         GAS const double* c;

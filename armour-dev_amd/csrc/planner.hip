@@ -1159,19 +1159,24 @@ int armour_device_compute_units(int device) {
     return n;
 }
 
-// streaming copy, 16 B per lane per access, four independent loads in flight per lane, grid-stride
-// (the achievable-HBM reference kernel)
-__global__ __launch_bounds__(256) void copy_kernel(const double2* __restrict__ src, double2* __restrict__ dst, long n) {
-    const long stride = (long)gridDim.x * blockDim.x;
-    long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const double2 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+// streaming copy (the achievable-HBM reference kernel): each workgroup copies one contiguous 16 KiB
+// block, four 16-B loads per lane in flight before its four stores, nontemporal both ways. Measured
+// shapes (tools/micro/copy.hip, 2 x 2 GiB): this one 5.9 TB/s; without nt 5.6; grid-stride with
+// four loads per lane (the round-4 kernel) 4.5; eight or sixteen per lane 4.3 / 5.2.
+typedef double copy_v2d __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void copy_kernel(const copy_v2d* __restrict__ src, copy_v2d* __restrict__ dst, long n) {
+    const long base = (long)blockIdx.x * 1024 + threadIdx.x;
+    copy_v2d v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const long i = base + k * 256;
+        if (i < n) v[k] = __builtin_nontemporal_load(&src[i]);
     }
-    for (; i < n; i += stride) dst[i] = src[i];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const long i = base + k * 256;
+        if (i < n) __builtin_nontemporal_store(v[k], &dst[i]);
+    }
 }
 
 double armour_copy_bandwidth(int device, size_t bytes, int reps) {
@@ -1184,16 +1189,14 @@ double armour_copy_bandwidth(int device, size_t bytes, int reps) {
     if (reps <= 0 || bytes < 16) return fail(ARMOUR_E_ARG, "bytes >= 16 and reps > 0");
     if (hipSetDevice(device) != hipSuccess) return fail(ARMOUR_E_HIP, "hipSetDevice failed (no device?)");
     const long n = (long)(bytes / 16);
-    double2 *a = nullptr, *b = nullptr;
+    copy_v2d *a = nullptr, *b = nullptr;
     hipEvent_t e0, e1;
     if (hipMalloc((void**)&a, n * 16) != hipSuccess) return fail(ARMOUR_E_HIP, "hipMalloc failed");
     if (hipMalloc((void**)&b, n * 16) != hipSuccess) { (void)hipFree(a); return fail(ARMOUR_E_HIP, "hipMalloc failed"); }
     (void)hipMemset(a, 0, n * 16);
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    int ncu = 256;
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-    const dim3 grid(ncu * 8), blk(256);
+    const dim3 grid((unsigned)((n + 1023) / 1024)), blk(256);
     hipLaunchKernelGGL(copy_kernel, grid, blk, 0, nullptr, a, b, n);
     (void)hipEventRecord(e0, nullptr);
     for (int r = 0; r < reps; r++) hipLaunchKernelGGL(copy_kernel, grid, blk, 0, nullptr, a, b, n);

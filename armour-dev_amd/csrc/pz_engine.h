@@ -33,6 +33,9 @@
 
 namespace armour {
 constexpr int MAX_SLOTS = 96;  // handle slots of a reach program (ProgramBuilder)
+#ifndef PZ_PREFIX_CHECK
+#define PZ_PREFIX_CHECK 0      // 1: arena_compact also forms the block offsets serially and reports mismatches
+#endif
 }
 
 #define AI __host__ __device__ inline __attribute__((always_inline))
@@ -633,23 +636,53 @@ AI void arena_compact(Ctx& x, int pc) {
     }
     g.sync();
     const int nb = misc[0];
-    if (g.tid == 0) {
-        // one thread: the sizes are independent loads, so the loop streams them (a parallel prefix,
-        // each thread summing the ranks below its own, gave wrong offsets on gfx950 while the host
-        // build of the same code was right; not kept)
-        long th0 = 0, tc0 = 0;
-        for (int r = 0; r < nb; r++) {
-            bnh[r] = th0;
-            bnc[r] = tc0;
-            if ((th0 != boh[r] || tc0 != boc[r]) && r < misc[1]) misc[1] = r;
-            th0 += bhc[r];
-            tc0 += bcc[r];
+    // New block offsets: a parallel prefix, each thread summing the sizes of the ranks below its own
+    // (16 independent table reads in flight). Round 4 replaced it by a one-thread loop after the
+    // LDS-arena test saw wrong offsets on the device; the cause was elsewhere (the room check in
+    // arena_ensure had no barrier behind it, so a wave could skip a compaction the others ran:
+    // DESIGN.md §4), and with that barrier the parallel and serial offsets agree bitwise on every
+    // compaction (PZ_PREFIX_CHECK=1 forms both and reports any difference).
+    for (int i = g.tid; i < nb; i += g.n) {
+        long sh = 0, sc = 0;
+        for (int r0 = 0; r0 < i; r0 += B) {
+            long hr[B], cr[B];
+            UNR for (int u = 0; u < B; u++) { const int r = min(r0 + u, MAX_SLOTS - 1); hr[u] = bhc[r]; cr[u] = bcc[r]; }
+            UNR for (int u = 0; u < B; u++) if (r0 + u < i) { sh += hr[u]; sc += cr[u]; }
         }
-        A.hused = th0;
-        A.cused = tc0;
+        bnh[i] = sh;
+        bnc[i] = sc;
+        if (sh != boh[i] || sc != boc[i]) int_min(&misc[1], i);
+        if (i == nb - 1) {
+            A.hused = sh + bhc[i];
+            A.cused = sc + bcc[i];
+        }
+    }
+    if (g.tid == 0) {
+        if (nb == 0) {
+            A.hused = 0;
+            A.cused = 0;
+        }
         A.ncompact++;
     }
     g.sync();
+#if PZ_PREFIX_CHECK
+    if (g.tid == 0) {
+        long th0 = 0, tc0 = 0;
+        int fs = MAX_SLOTS;
+        for (int r = 0; r < nb; r++) {
+            if (bnh[r] != th0 || bnc[r] != tc0)
+                printf("prefix mismatch: block %d pc %d rank %d of %d: parallel (%ld, %ld) serial (%ld, %ld)\n",
+                       (int)blockIdx.x, pc, r, nb, bnh[r], bnc[r], th0, tc0);
+            if ((th0 != boh[r] || tc0 != boc[r]) && r < fs) fs = r;
+            th0 += bhc[r];
+            tc0 += bcc[r];
+        }
+        if (fs != misc[1] || th0 != A.hused || tc0 != A.cused)
+            printf("prefix mismatch: block %d pc %d first %d / %d, used (%ld, %ld) / (%ld, %ld)\n", (int)blockIdx.x, pc,
+                   misc[1], fs, A.hused, A.cused, th0, tc0);
+    }
+    g.sync();
+#endif
     const int first = misc[1];
     const long th = A.hused, tc = A.cused;
     if (g.tid == 0 && first < nb) A.cmoved += tc - bnc[first];

@@ -129,12 +129,20 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
     // fallen below 0.9999 x the largest of the last 4 reference values, and back to free mode once
     // it has (Ipopt: adaptive_mu_globalization kkt-error, kkterror_red_iters 4, red_fact 0.9999,
     // adaptive_mu_monotone_init_factor 0.8, mu_oracle loqo)
-    bool free_mode = opt.mu_strategy == 1;
+    bool free_mode = opt.mu_strategy >= 1;
     std::vector<double> kkt_ref;
+    // mu_strategy 2 (study only): Ipopt's default adaptive pair, mu_oracle quality-function with
+    // adaptive_mu_globalization obj-constr-filter (qf_mu below); the filter of (f, theta) of the
+    // free-mode iterates, and Ipopt's mu bounds (mu_min 1e-11, mu_max = min(1e5, 1e3 avg(s z) at the start))
+    std::vector<double> gf_f, gf_t;
+    double mu_max_qf = -1;
     // the adaptive rule's floor: tol / 10, the monotone rule's floor (Ipopt's mu_min default is
     // 1e-11; below ~tol / 10 the reduced system's Sigma = z / s ~ z^2 / mu of the active rows makes
     // the 1e-4-tolerance solution reproducible to ~1e-5 only: DESIGN.md §5, tools/mu_sensitivity.py)
-    const double mu_min = (opt.mu_study & 2) ? 1e-11 : opt.tol / 10;
+    // mu_strategy 3 (study only): the quality-function pair with the product's floor tol / 10 and grid
+    const bool qf = opt.mu_strategy == 2 || opt.mu_strategy == 3;
+    const double mu_min = (opt.mu_study & 2) || opt.mu_strategy == 2 ? 1e-11 : opt.tol / 10;
+    auto qf_grid = [&](double v) { return opt.mu_strategy == 3 ? mu_grid(v) : v; };
     IpmResult res{1, 0, 0, 0.0, 0.0, -1};
     double a[NMAX], at[NMAX];
     int it;
@@ -242,6 +250,99 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             iter++;
         }
     };
+    // the quality-function oracle's sigma at the current iterate (mu_strategy 2 only): reads the
+    // dual residual rd_q and the slack residuals rplo / rphi of step 1
+    double rd_q[NMAX];
+    auto qf_sigma = [&](double avg) -> double {
+        double M[NMAX * NMAX], b0[NMAX], b1[NMAX], dx0[NMAX], dx1[NMAX];
+        for (int i = 0; i < n * n; i++) M[i] = H[i];
+        for (int j = 0; j < n; j++) { b0[j] = -grad[j]; b1[j] = 0; }
+        for (int r = 0; r < R; r++) {
+            grow(J, r, a);
+            double sig = 0, c0 = 0, c1 = 0;
+            if (hlo[r]) { const double sr = zlo[r] / slo[r]; sig += sr; c0 -= sr * rplo[r]; c1 += 1.0 / slo[r]; }
+            if (hhi[r]) { const double sr = zhi[r] / shi[r]; sig += sr; c0 += sr * rphi[r]; c1 -= 1.0 / shi[r]; }
+            for (int i = 0; i < n; i++) {
+                b0[i] += a[i] * c0;
+                b1[i] += a[i] * c1;
+                for (int j = 0; j < n; j++) M[i * n + j] += sig * a[i] * a[j];
+            }
+        }
+        double shift = 0.0;
+        bool ok = false;
+        for (int tries = 0; tries < 40 && !ok; tries++) {
+            ok = chol_solve(M, n, shift, b0, dx0) && chol_solve(M, n, shift, b1, dx1);
+            shift = (shift == 0.0) ? 1e-8 : shift * 10;
+        }
+        if (!ok) return 0.1;
+        std::vector<double> adx0(R), adx1(R);
+        for (int r = 0; r < R; r++) {
+            grow(J, r, a);
+            double u0 = 0, u1 = 0;
+            for (int j = 0; j < n; j++) { u0 += a[j] * dx0[j]; u1 += a[j] * dx1[j]; }
+            adx0[r] = u0;
+            adx1[r] = u1;
+        }
+        double nd = 0, np = 0;
+        for (int j = 0; j < n; j++) nd += rd_q[j] * rd_q[j];
+        int ns = 0;
+        for (int r = 0; r < R; r++) {
+            if (hlo[r]) { np += rplo[r] * rplo[r]; ns++; }
+            if (hhi[r]) { np += rphi[r] * rphi[r]; ns++; }
+        }
+        nd /= std::max(1, n);
+        np /= std::max(1, ns);
+        auto q = [&](double sg) {
+            const double mu_s = sg * avg;
+            const double tau = std::max(opt.tau_min, 1.0 - mu_s);
+            double ap = 1.0, ad = 1.0;
+            for (int r = 0; r < R; r++) {
+                const double adx = adx0[r] + mu_s * adx1[r];
+                if (hlo[r]) {
+                    const double ds = adx + rplo[r], dz = mu_s / slo[r] - zlo[r] - zlo[r] / slo[r] * ds;
+                    if (ds < 0) ap = std::min(ap, -tau * slo[r] / ds);
+                    if (dz < 0) ad = std::min(ad, -tau * zlo[r] / dz);
+                }
+                if (hhi[r]) {
+                    const double ds = -adx + rphi[r], dz = mu_s / shi[r] - zhi[r] - zhi[r] / shi[r] * ds;
+                    if (ds < 0) ap = std::min(ap, -tau * shi[r] / ds);
+                    if (dz < 0) ad = std::min(ad, -tau * zhi[r] / dz);
+                }
+            }
+            double cc = 0;
+            for (int r = 0; r < R; r++) {
+                const double adx = adx0[r] + mu_s * adx1[r];
+                if (hlo[r]) {
+                    const double ds = adx + rplo[r], dz = mu_s / slo[r] - zlo[r] - zlo[r] / slo[r] * ds;
+                    const double c = (slo[r] + ap * ds) * (zlo[r] + ad * dz);
+                    cc += c * c;
+                }
+                if (hhi[r]) {
+                    const double ds = -adx + rphi[r], dz = mu_s / shi[r] - zhi[r] - zhi[r] / shi[r] * ds;
+                    const double c = (shi[r] + ap * ds) * (zhi[r] + ad * dz);
+                    cc += c * c;
+                }
+            }
+            return (1 - ad) * (1 - ad) * nd + (1 - ap) * (1 - ap) * np + cc / std::max(1, ns);
+        };
+        const double smin = std::max(1e-6, mu_min / avg), smax = std::min(100.0, mu_max_qf / avg);
+        const double q1 = q(1.0);
+        const bool up = q(1.0 - 1e-4) > q1;  // q decreases towards sigma > 1
+        const double gr = 0.5 * (std::sqrt(5.0) - 1.0);
+        // golden section on [lo, hi] (log scale below 1), at most 8 steps
+        double lo = up ? 1.0 : std::log(std::min(smin, 1.0)), hi = up ? std::max(smax, 1.0) : 0.0;
+        auto sig_of = [&](double t) { return up ? t : std::exp(t); };
+        double m1 = hi - gr * (hi - lo), m2 = lo + gr * (hi - lo);
+        double f1 = q(sig_of(m1)), f2 = q(sig_of(m2));
+        for (int k = 0; k < 8; k++) {
+            if (sig_of(hi) - sig_of(lo) < 1e-2 * sig_of(hi)) break;
+            if (f1 <= f2) { hi = m2; m2 = m1; f2 = f1; m1 = hi - gr * (hi - lo); f1 = q(sig_of(m1)); }
+            else { lo = m1; m1 = m2; f1 = f2; m2 = lo + gr * (hi - lo); f2 = q(sig_of(m2)); }
+        }
+        double best = f1 <= f2 ? sig_of(m1) : sig_of(m2), fb = std::min(f1, f2);
+        if (q1 < fb) best = 1.0;
+        return std::min(std::max(best, smin), std::max(smax, smin));
+    };
     for (it = 0; it < opt.max_iter; it++) {
         // 1. residuals and errors
         double rd[NMAX];
@@ -272,6 +373,7 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
         }
         double inf_d = 0;
         for (int j = 0; j < n; j++) inf_d = std::max(inf_d, std::fabs(rd[j]));
+        for (int j = 0; j < n; j++) rd_q[j] = rd[j];
         const double sd = std::max(opt.s_max, sumz / std::max(1, nside)) / opt.s_max;
         const double E0 = std::max(std::max(inf_d / sd, inf_p), compl0 / sd);
         res.kkt_error = E0;
@@ -286,7 +388,49 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             }
             Emu = std::max(std::max(inf_d / sd, inf_p), cm / sd);
         }
-        if (opt.mu_strategy == 1) {
+        if (qf) {
+            // Ipopt's default adaptive pair (IpAdaptiveMuUpdate.cpp, IpQualityFunctionMuOracle.cpp
+            // with their default options), restated for the pricing study of DESIGN.md §5:
+            //   globalisation obj-constr-filter: in free mode the iterate must be acceptable to a
+            //   filter of the earlier free-mode iterates' (f, theta) with margin 1e-5 min(1, theta)
+            //   (filter_margin_fact, filter_max_margin); else fixed (monotone) mode from
+            //   0.8 avg(s z) (adaptive_mu_monotone_init_factor), back to free mode once acceptable;
+            //   oracle quality-function: mu = sigma avg(s z), sigma minimising the quality function
+            //   q = (1 - a_D)^2 |r_d|^2 / n_d + (1 - a_P)^2 |r_p|^2 / n_p + |(s + a_P ds)(z + a_D dz)|^2 / n_c
+            //   (quality_function_norm_type 2-norm-squared, no centrality or balancing term) of the
+            //   step dx(mu) = dx_aff + mu dx_1 with fraction-to-boundary step sizes a_P, a_D,
+            //   by golden section (at most 8 steps, sigma tolerance 1e-2) on [sigma_min = 1e-6, 1] in
+            //   log scale or [1, sigma_max = 100], whichever side q decreases into from sigma = 1.
+            double sum = 0, theta = 0;
+            for (int r = 0; r < R; r++) {
+                if (hlo[r]) { sum += slo[r] * zlo[r]; theta += std::fabs(rplo[r]); }
+                if (hhi[r]) { sum += shi[r] * zhi[r]; theta += std::fabs(rphi[r]); }
+            }
+            const double avg = sum / std::max(1, nside);
+            if (mu_max_qf < 0) mu_max_qf = std::min(1e5, 1e3 * avg);
+            const double margin = 1e-5 * std::min(1.0, theta);
+            bool acceptable = true;
+            for (size_t q = 0; q < gf_f.size(); q++)
+                if (!(f + margin < gf_f[q] || theta + margin < gf_t[q])) acceptable = false;
+            const double mu_old = mu;
+            if (free_mode && !acceptable) {
+                free_mode = false;
+                mu = std::max(mu_min, qf_grid(0.8 * avg));
+            } else if (!free_mode && acceptable) {
+                free_mode = true;
+            }
+            if (free_mode) {
+                gf_f.push_back(f);
+                gf_t.push_back(theta);
+                mu = std::max(mu_min, std::min(qf_grid(qf_sigma(avg) * avg), mu_max_qf));
+            } else if (Emu <= opt.kappa_eps * mu && mu > mu_min) {
+                mu = std::max(mu_min, std::min(opt.kappa_mu * mu, std::pow(mu, opt.theta_mu)));
+            }
+            if (mu != mu_old) {
+                filt_theta.clear();
+                filt_phi.clear();
+            }
+        } else if (opt.mu_strategy == 1) {
             // adaptive (Ipopt's mu_strategy "adaptive", KPR/Parameters.h:57): free mode takes mu
             // from the LOQO oracle, sigma = 0.1 min(0.05 (1 - xi) / xi, 2)^3 with xi = min(s z) /
             // avg(s z); the kkt-error globalisation switches to fixed (monotone) mode, from
@@ -447,8 +591,10 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             theta_max = -1;
             theta_min = -1;
             nfail = 0;
-            free_mode = opt.mu_strategy == 1;
+            free_mode = opt.mu_strategy >= 1;
             kkt_ref.clear();
+            gf_f.clear();
+            gf_t.clear();
             it--;  // (the loop's increment; restoration counted its own iterations)
             continue;
         }

@@ -41,7 +41,9 @@ struct IpmOptions {
     // barrier strategy: 1 adaptive (the default: the reference's IPOPT_MU_STRATEGY "adaptive",
     // KPR/Parameters.h:57, restated with Ipopt's mu_oracle loqo and adaptive_mu_globalization
     // kkt-error — not Ipopt's default quality-function / obj-constr-filter pair — with mu on a
-    // 2^(1/8) grid and the floor tol / 10; ipm.cpp); 0 monotone (Fiacco-McCormick)
+    // 2^(1/8) grid and the floor tol / 10; ipm.cpp); 0 monotone (Fiacco-McCormick);
+    // 2 (pricing study only, not on the device): Ipopt's default adaptive pair, mu_oracle
+    // quality-function and adaptive_mu_globalization obj-constr-filter, with Ipopt's mu_min 1e-11
     int mu_strategy = 1;
     // studies of the adaptive rule only (tools/mu_sensitivity.py): bit 0 drops the 2^(1/8) grid
     // (ipm.cpp mu_grid), bit 1 the tol / 10 floor (Ipopt's mu_min 1e-11 instead)

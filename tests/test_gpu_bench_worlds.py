@@ -92,7 +92,8 @@ def test_bench_step_matches_oracle_world_by_world():
 
 def test_single_world_plans_match_oracle():
     """The drop-in's batch — one world per call — takes other paths than the bench step: the
-    per-job reach engine on its LDS arena (reach_kernel<256, true>), the sync-free tail from the
+    per-job reach engine (reach_kernel<256>, the HBM arena by default; the LDS-arena form
+    reach_kernel<256, true> is opt-in, ARMOUR_LDS_ARENA=1), the sync-free tail from the
     second iteration, and restoration phases after the interior-point loop. The first 48 headline
     worlds planned one at a time against the same frozen oracle plans: every decision identical,
     and the solver's path (iterations, k_opt within 1e-8 when converged or feasible) for all but
