@@ -328,7 +328,7 @@ class Planner:
 
     def plane_cache_stats(self):
         """certified plane cache of the current reach sets (armour_get_plane_cache_stats)"""
-        keys = ("planes_kept", "pairs", "blocks_cached", "blocks", "max_per_pair", "records_per_block", "box_misses")
+        keys = ("planes_kept", "pairs", "blocks_cached", "blocks", "max_per_pair", "pool_records", "box_misses")
         out = (ctypes.c_longlong * len(keys))()
         _check(min(0, lib().armour_get_plane_cache_stats(self.h, out, len(keys))))
         return {k: int(out[i]) for i, k in enumerate(keys)}

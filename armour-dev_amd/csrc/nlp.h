@@ -156,20 +156,24 @@ struct NlpDev {
     // Certified plane cache (plane_cache_kernel). The 36 planes of a buffered
     // obstacle and their offsets d, delta do not depend on x; only A . c(x) does. For every
     // (world, t, link, obstacle) the cache holds the planes that can attain the maximum for some x in
-    // the box |x_i| <= PC_XBOX, in the reference's scan order: (world, t) region of pc_cap records
-    // [5][pc_cap] (A0 A1 A2, P = d + delta, N = -d + delta), pcoff [W][T][NJ * O] = (first record << 8)
-    // | count, pcok [W][T] = 1 when the region held every survivor (always: pc_cap has room for all
-    // 36 planes of every pair; reads touch only the records kept, ~5 per pair).
+    // the box |x_i| <= PC_XBOX, in the reference's scan order. The records of a (world, t) block are
+    // n = its kept-plane count contiguous records at pcbase[w][t] of one pool: [5][n] (A0 A1 A2,
+    // P = d + delta, N = -d + delta) from pc + 5 pcbase, the pair (l * O + o) of each from
+    // pcp + pcbase; pcoff [W][T][NJ * O] = (first record << 8) | count; pcok [W][T] = 1 when the pool
+    // held the block (the host sizes the pool from the count every build needed, ensure_plane_cache,
+    // so a build that ran out is repeated on a larger pool and every block is cached).
     int pcache;             // cache enabled (ARMOUR_PLANE_CACHE=0 disables it)
     int pcready;            // built for the current reach sets and obstacles
-    int pc_cap;             // records per (world, t)
-    double* pc;
-    uint16_t* pcp;          // [W][T][pc_cap]: the pair (l * O + o) of each record
+    long pc_pool;           // records in the pool
+    double* pc;             // [5 pc_pool]
+    uint16_t* pcp;          // [pc_pool]
     unsigned* pcoff;
     unsigned char* pcok;
+    unsigned long long* pcbase;  // [W][T] first pool record of each block
+    unsigned* pcnext;            // pool records handed out by the current build (zeroed by jrs_kernel)
 };
 constexpr int EV_MAXK = 9;   // speculative trials per world (max_ls - 1)
-constexpr int PC_K = COMB;             // cache records per pair reserved: all 36 planes
+constexpr int PC_K = 12;               // initial pool: records per pair per block (ARMOUR_PC_K; the survey workload keeps 5.3)
 constexpr double PC_XBOX = 1.0 + 1e-6; // certified box of x (the solver keeps |x_i| <= 1)
 constexpr double PC_RADF = 1.0001;     // >= PC_XBOX^21, the largest monomial degree sum (7 x 3)
 constexpr double PC_MARGIN = 1e-9;     // >> the rounding of the bound and of A . c (~1e-15)

@@ -586,12 +586,21 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
         if (tid == 63) total_s = incl;
     }
     __syncthreads();
-    const bool ok = total_s <= (unsigned)d.pc_cap;
-    if (tid == 0) d.pcok[jt] = ok ? 1 : 0;
-    if (!ok) return;
-    double* const rec = d.pc + jt * 5 * d.pc_cap;
-    uint16_t* const pcp = d.pcp + jt * d.pc_cap;
-    const int cap = d.pc_cap;
+    // the block's records from the pool: one atomic per block; a build that runs out of pool is
+    // repeated by the host on a larger one (ensure_plane_cache)
+    __shared__ unsigned long long base_s;
+    if (tid == 0) {
+        const unsigned long long b0 = atomicAdd(d.pcnext, total_s);
+        const bool fits = b0 + total_s <= (unsigned long long)d.pc_pool;
+        d.pcok[jt] = fits ? 1 : 0;
+        d.pcbase[jt] = fits ? b0 : 0;
+        base_s = fits ? b0 : ~0ull;
+    }
+    __syncthreads();
+    if (base_s == ~0ull) return;
+    double* const rec = d.pc + 5 * base_s;
+    uint16_t* const pcp = d.pcp + base_s;
+    const int cap = (int)total_s;  // the block's [5][n] record arrays
     for (int pr = tid; pr < NP; pr += blockDim.x) {
         const int l = pr / O, o = pr % O;
         double G[BUF_GEN][3], oc[3];
@@ -879,11 +888,12 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
             // strict-> first maximum, value, plane and sign exactly. The pair tables live in the
             // slicing buffer (free now).
             const int NP = NJ * O;
-            const double* const rec = d.pc + jt * 5 * d.pc_cap;
-            const uint16_t* const pcp = d.pcp + jt * d.pc_cap;
-            const int cap = d.pc_cap;
             const unsigned last = d.pcoff[jt * NP + NP - 1];
             const int total = (int)(last >> 8) + (int)(last & 255);
+            const unsigned long long pb = d.pcbase[jt];
+            const double* const rec = d.pc + 5 * pb;
+            const uint16_t* const pcp = d.pcp + pb;
+            const int cap = total;  // the block's [5][n] record arrays
             // eval_pair_doubles(NP) <= UB: always for UB_FULL, checked by the host for UB_S
             unsigned long long* const pkey = reinterpret_cast<unsigned long long*>(ubuf);  // [NP]
             unsigned* const pidx = reinterpret_cast<unsigned*>(ubuf + NP);                   // [NP]
@@ -1295,11 +1305,12 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     // every thread takes records straight from global memory and forms each trial's two candidates;
     // the (trial, pair) maximum by an LDS atomicMax on an order-preserving key (the value is all a
     // trial needs; a +-0 tie cannot change the line search's terms). Tables in the slicing buffer.
-    const double* const rec = d.pc + jt * 5 * d.pc_cap;
-    const uint16_t* const pcp = d.pcp + jt * d.pc_cap;
-    const int cap = d.pc_cap;
     const unsigned last = NP > 0 ? d.pcoff[jt * NP + NP - 1] : 0u;
     const int total = (int)(last >> 8) + (int)(last & 255);
+    const unsigned long long pb = d.pcbase[jt];
+    const double* const rec = d.pc + 5 * pb;
+    const uint16_t* const pcp = d.pcp + pb;
+    const int cap = total;  // the block's [5][n] record arrays
     unsigned long long* const pkey = reinterpret_cast<unsigned long long*>(ubuf);  // [K][NP]
     static_assert(EV_MAXK * MAX_J * MAX_OBS <= UB_FULL, "trial pair table");  // K * NP <= UB_TS: host check
     const double start = -100000000.0;

@@ -122,6 +122,7 @@ struct armour_planner {
     WorldState* h_ws = nullptr;
     double* h_f = nullptr;
     int* h_feas = nullptr;
+    unsigned* h_pcnext = nullptr;  // pinned: the plane cache pool records the last build needed
     // state of the last batch
     int W = 0, O = 0;
     bool reached = false, planned = false;
@@ -475,14 +476,29 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // active-world lists: two per iteration (ping-pong), two per line-search round
     // (+ two for the restoration phases inside the interior-point loop)
     if ((rc = p->alloc(&p->d_lists, 6 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 16))) return rc;
-    // certified plane cache: room for all 36 planes of every (link, obstacle) pair of every (world, t)
+    // certified plane cache: a region of PC_K records per (link, obstacle) pair for every (world, t)
+    // (ARMOUR_PC_K, 1..36). The survey workload keeps 5.3 planes per pair on average; a (world, t)
+    // whose kept planes exceed its region is flagged (pcok) and evaluated by the full scan, with
+    // bitwise the same results, so the region size trades memory for speed only. Round 4 reserved
+    // all 36 (42 MB per world at T = 100, O = 20), which capped the batch a GPU can hold.
     d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
     d.pcready = 0;
-    d.pc_cap = PC_K * NJ * Om;
-    if (d.pcache && ((rc = p->alloc(&d.pc, jobs * 5 * (size_t)d.pc_cap)) || (rc = p->alloc(&d.pcp, jobs * (size_t)d.pc_cap)) ||
-                     (rc = p->alloc(&d.pcoff, jobs * NJ * (size_t)Om)) ||
-                     (rc = p->alloc(&d.pcok, jobs))))
+    {
+        const char* pk = std::getenv("ARMOUR_PC_K");
+        const int k = pk ? std::atoi(pk) : PC_K;
+        d.pc_pool = std::max(1L, (long)std::min(std::max(k, 1), COMB) * NJ * std::max(Om, 1) * (long)jobs);
+    }
+    if (d.pcache && ((rc = p->alloc(&d.pc, 5 * (size_t)d.pc_pool)) || (rc = p->alloc(&d.pcp, (size_t)d.pc_pool)) ||
+                     (rc = p->alloc(&d.pcoff, jobs * NJ * (size_t)Om)) || (rc = p->alloc(&d.pcok, jobs)) ||
+                     (rc = p->alloc(&d.pcbase, jobs)) || (rc = p->alloc(&d.pcnext, 1))))
         return rc;
+    if (d.pcache) {
+        HIPCK(hipMemset(d.pcnext, 0, sizeof(unsigned)));
+        HIPCK(hipHostMalloc((void**)&p->h_pcnext, sizeof(unsigned)));
+        p->rc.pc_next = d.pcnext;
+        p->ra.rc.pc_next = d.pcnext;
+        p->la.rc.pc_next = d.pcnext;
+    }
     // speculative line-search slots (values only): every world x (max_ls - 1) trials. The speculative
     // round reads the plane cache (ARMOUR planner, fp64); otherwise the rounds run one by one.
     d.K = d.opt.max_ls - 1;
@@ -759,7 +775,31 @@ static int run_reach(armour_planner* p) {
 static void ensure_plane_cache(armour_planner* p) {
     NlpDev& d = p->d;
     if (!d.pcache || d.pcready || d.O == 0 || p->eval_f32) return;
-    hipLaunchKernelGGL(plane_cache_kernel, dim3(p->T, p->W), dim3(EVAL_THREADS), 0, p->stream, d);
+    // The pool is sized at creation for ARMOUR_PC_K records per pair; a build whose blocks need
+    // more (the count is known only on the device) is repeated on a pool of 1.25x what it needed,
+    // so every block is cached. One host wait on the build, which the solver's first kernels wait
+    // for anyway.
+    for (int attempt = 0; attempt < 2; attempt++) {
+        hipLaunchKernelGGL(plane_cache_kernel, dim3(p->T, p->W), dim3(EVAL_THREADS), 0, p->stream, d);
+        if (hipMemcpyAsync(p->h_pcnext, d.pcnext, sizeof(unsigned), hipMemcpyDeviceToHost, p->stream) != hipSuccess ||
+            hipStreamSynchronize(p->stream) != hipSuccess)
+            break;
+        const long need = (long)*p->h_pcnext;
+        if (need <= d.pc_pool) break;
+        const long grow = need + need / 4;
+        double* pc = nullptr;
+        uint16_t* pcp = nullptr;
+        if (dalloc(&pc, 5 * (size_t)grow) != hipSuccess) break;
+        if (dalloc(&pcp, (size_t)grow) != hipSuccess) { (void)hipFree(pc); break; }
+        for (void*& a : p->allocs) {
+            if (a == (void*)d.pc) { (void)hipFree(a); a = pc; }
+            else if (a == (void*)d.pcp) { (void)hipFree(a); a = pcp; }
+        }
+        d.pc = pc;
+        d.pcp = pcp;
+        d.pc_pool = grow;
+        (void)hipMemsetAsync(d.pcnext, 0, sizeof(unsigned), p->stream);
+    }
     d.pcready = 1;
 }
 
@@ -1267,6 +1307,7 @@ void armour_destroy(armour_planner* p) {
     if (p->h_ws) (void)hipHostFree(p->h_ws);
     if (p->h_f) (void)hipHostFree(p->h_f);
     if (p->h_feas) (void)hipHostFree(p->h_feas);
+    if (p->h_pcnext) (void)hipHostFree(p->h_pcnext);
     if (p->stream) {
         for (int i = 0; i < 6; i++) (void)hipEventDestroy(p->ev[i]);
         for (int i = 0; i < 2; i++) (void)hipEventDestroy(p->tev[i]);
@@ -1558,7 +1599,7 @@ int armour_get_plane_cache_stats(armour_planner* p, long long* out, int n) {
     for (unsigned char v : ok) nok += v;
     unsigned miss = 0;
     HIPCK(hipMemcpy(&miss, d.cnt + 7, sizeof(unsigned), hipMemcpyDeviceToHost));
-    const long long st[ARMOUR_PC_COUNT] = {kept, (long long)off.size(), nok, (long long)blocks, mx, d.pc_cap, miss};
+    const long long st[ARMOUR_PC_COUNT] = {kept, (long long)off.size(), nok, (long long)blocks, mx, d.pc_pool, miss};
     for (int k = 0; k < n && k < ARMOUR_PC_COUNT; k++) out[k] = st[k];
     return ARMOUR_PC_COUNT;
 }

@@ -54,6 +54,7 @@ struct ReachCounters {
     unsigned* done;             // [1] workgroups finished (the last one resets it to 0)
     long long* hsum;            // mapped host [RSUM_ERR + W]
     long long seq;              // this launch's sequence number (planner.hip run_reach)
+    unsigned* pc_next;          // the plane cache pool counter of the solver (NlpDev::pcnext; may be null)
 };
 
 __device__ inline void zero_counters(const ReachCounters& c, int* err, int W) {
@@ -61,6 +62,7 @@ __device__ inline void zero_counters(const ReachCounters& c, int* err, int W) {
     for (int k = threadIdx.x; k < W; k += blockDim.x) err[k] = 0;
     if (threadIdx.x < 8) c.occ[threadIdx.x] = 0;
     if (threadIdx.x == 0) *c.bytes = 0;
+    if (threadIdx.x == 0 && c.pc_next) *c.pc_next = 0;
 }
 
 // after a workgroup's last job: the last workgroup of the grid copies the counters out (reads

@@ -212,7 +212,7 @@ int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms
 /* Certified plane cache of the current reach sets, built on demand: for k < n
  * writes [0] planes kept over all (world, t, link, obstacle) pairs, [1] pairs, [2] (world, t) blocks
  * whose cache region held every kept plane, [3] blocks, [4] most planes kept for one pair,
- * [5] records per block region, [6] evaluations that found a point outside the cache's box (rows
+ * [5] records in the cache pool, [6] evaluations that found a point outside the cache's box (rows
  * NaN; the solver never produces one). Returns ARMOUR_PC_COUNT; ARMOUR_E_STATE when the cache is off. */
 #define ARMOUR_PC_COUNT 7
 int armour_get_plane_cache_stats(armour_planner* p, long long* out, int n);

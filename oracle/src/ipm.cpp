@@ -326,6 +326,17 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             return (1 - ad) * (1 - ad) * nd + (1 - ap) * (1 - ap) * np + cc / std::max(1, ns);
         };
         const double smin = std::max(1e-6, mu_min / avg), smax = std::min(100.0, mu_max_qf / avg);
+        if (opt.qf_grid > 0) {
+            // the device's form (study): q on a fixed log grid of sigma over [1e-6, 100], argmin
+            // (first of equals), clipped to [smin, smax]
+            double best = 1.0, fb = 1e300;
+            for (int k = 0; k < opt.qf_grid; k++) {
+                const double sg = std::pow(10.0, -6.0 + 8.0 * k / (opt.qf_grid - 1));
+                const double fq = q(sg);
+                if (fq < fb) { fb = fq; best = sg; }
+            }
+            return std::min(std::max(best, smin), std::max(smax, smin));
+        }
         const double q1 = q(1.0);
         const bool up = q(1.0 - 1e-4) > q1;  // q decreases towards sigma > 1
         const double gr = 0.5 * (std::sqrt(5.0) - 1.0);

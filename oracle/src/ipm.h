@@ -45,6 +45,7 @@ struct IpmOptions {
     // 2 (pricing study only, not on the device): Ipopt's default adaptive pair, mu_oracle
     // quality-function and adaptive_mu_globalization obj-constr-filter, with Ipopt's mu_min 1e-11
     int mu_strategy = 1;
+    int qf_grid = 0;  // mu_strategy 2 / 3 studies: > 0 replaces the golden section by a fixed grid of this many sigmas
     // studies of the adaptive rule only (tools/mu_sensitivity.py): bit 0 drops the 2^(1/8) grid
     // (ipm.cpp mu_grid), bit 1 the tol / 10 floor (Ipopt's mu_min 1e-11 instead)
     int mu_study = 0;

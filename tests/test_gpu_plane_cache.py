@@ -95,3 +95,20 @@ def test_plane_cache_stats_survey():
     assert st["pairs"] == W * T * 7 * O
     assert st["blocks_cached"] == st["blocks"]
     assert 1 <= st["max_per_pair"] <= 36
+
+
+def test_plane_cache_pool_regrows():
+    """The cache's records live in one pool sized at creation for ARMOUR_PC_K records per pair
+    (default 12; the survey workload keeps 5.3). A pool too small for a build (ARMOUR_PC_K=1) is
+    grown to what the build needed and the build repeated: every block cached, and the plans and
+    constraint values bitwise those of the default pool and of the full scan."""
+    T, O, W = 100, 20, 8
+    worlds = [A.make_world(3000 + s, O, profile="survey") for s in range(W)]
+    P, Q = planners(T, O, W)
+    with env("ARMOUR_PC_K", "1"):
+        S = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    S.reach(worlds)
+    st = S.plane_cache_stats()
+    assert st["blocks_cached"] == st["blocks"] and st["pool_records"] >= st["planes_kept"] > W * T * 7 * O
+    check_plan(S, Q, worlds)
+    check_plan(P, S, worlds)

@@ -14,6 +14,13 @@
 #                       SCRIPT may also be a built executable (tools/micro/...), run directly
 #   traffic TAG BATCH   FETCH_SIZE and WRITE_SIZE passes over one bench step, then tools/pmc_traffic.py
 #                       writes gpurun_out/<TAG>_reach_traffic.json for this library build
+#   sweep 'ARGS' V...   bench.py ARGS once per value V, "{}" in ARGS replaced by V (planner counts,
+#                       batch sizes; an env sweep: 'env ARMOUR_ROW_CHUNK={} ...' is not supported,
+#                       put the variable in ARGS as --flag or use envab); one line per value
+#   libab VARIANT RE    one planner's solver timeline (tools/nlp_trace.py, 327 survey worlds) under
+#                       rocprofv3 with the in-tree library and with armour_amd/VARIANT, twice each,
+#                       iteration profile and the kernels matching RE (same-box A/B)
+#   envab NAME V0 V1 RE the same timeline A/B between two values of environment variable NAME
 # Environment for a step: prefix it, e.g. 'env ARMOUR_ENGINE=job py tools/reach_time.py 32'.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -68,6 +75,25 @@ for step in "$@"; do
       python3 tools/pmc_traffic.py "$OUT/${tag}_fetch/run_counter_collection.csv" "$OUT/${tag}_write/run_counter_collection.csv" \
           lane_reach_kernel "$OUT/${ttag}_reach_traffic.json" "$ttag" "$batch" survey
       rc=$?; [ $rc -eq 0 ] && cat "$OUT/${ttag}_reach_traffic.json" ;;
+    sweep)
+      args=$1; shift; rc=0
+      for v in "$@"; do
+        env "${envs[@]}" timeout -k 10 600 python3 bench.py ${args//\{\}/$v} > "$OUT/${tag}_$v.json" 2> "$OUT/${tag}_$v.err" || { rc=$?; break; }
+        python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value'], 1), round(d['ms_per_step'], 2), {k: round(v, 2) for k, v in d['breakdown_ms'].items()})" "$OUT/${tag}_$v.json" "$v"
+      done ;;
+    libab|envab)
+      rc=0; mkdir -p "$OUT/$tag"
+      if [ "$kind" = libab ]; then names=(libarmour_hip.so "$1"); re=$2; else names=("$2" "$3"); re=$4; fi
+      for rep in 1 2; do
+        for nm in "${names[@]}"; do
+          if [ "$kind" = libab ]; then ev=(ARMOUR_LIB="$R/armour-dev_amd/armour_amd/$nm"); else ev=("$1=$nm"); fi
+          (cd /tmp && env "${envs[@]}" "${ev[@]}" timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv \
+              -d "$OUT/$tag/$nm.$rep" -o run -- python3 "$R/tools/nlp_trace.py" survey 327) > "$OUT/$tag/$nm.$rep.log" 2>&1 || { rc=$?; break 2; }
+          echo "== $nm (rep $rep)"
+          python3 tools/iter_profile.py "$OUT/$tag/$nm.$rep/run_kernel_trace.csv" | sed -n 1,1p
+          python3 tools/trace_summary.py "$OUT/$tag/$nm.$rep/run_kernel_trace.csv" | grep -E "$re"
+        done
+      done ;;
     *)
       echo "unknown step kind: $kind"; rc=2 ;;
   esac

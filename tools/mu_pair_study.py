@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 
 STRATEGY = int(os.environ.get("MU_STRATEGY", "2"))
+QF_GRID = int(os.environ.get("QF_GRID", "0"))  # > 0: sigma from a fixed log grid (the device-friendly form)
 
 
 def plan(seed):
@@ -31,7 +32,7 @@ def plan(seed):
 
     R = OraclePlanner(*A.make_world(seed, 20, profile="survey"), T=100, threads=1)
     R.reach()
-    r = R.plan(mu_strategy=STRATEGY)
+    r = R.plan(mu_strategy=STRATEGY, flags=QF_GRID << 8)
     return seed, r["feasible"], r["status"], r["iterations"], r["evaluations"], r["k_opt"], r["cost"]
 
 
@@ -84,7 +85,10 @@ def main():
         "seconds": round(time.time() - t0, 1),
     }
     out["mu_strategy"] = STRATEGY
-    path = os.path.join(ROOT, "profiles", "r05_mu_pair_study.json" if STRATEGY == 2 else f"r05_mu_pair_study_s{STRATEGY}.json")
+    out["qf_grid"] = QF_GRID
+    tag = "" if STRATEGY == 2 else f"_s{STRATEGY}"
+    tag += f"_g{QF_GRID}" if QF_GRID else ""
+    path = os.path.join(ROOT, "profiles", f"r05_mu_pair_study{tag}.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
