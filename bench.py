@@ -9,7 +9,7 @@ intersect the start configuration), so a share of the worlds is infeasible and t
 against active constraints; the line reports the feasible fraction.
 
 Modes
-  weak (default): every rank plans its own --batch worlds per planner per step (default: two
+  weak (default): every rank plans its own --batch worlds per planner per step (default: eight
       whole waves of 64-job reach bundles); `value` = all ranks' worlds / max-over-ranks step time.
   strong (--total-worlds N, config 4): one fixed job of N worlds sharded over the ranks
       (armour_amd.dist.shard), each rank's shard split over its planners.
@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
-                    help="worlds per planner per step (0: two whole bundle waves of the device, floor(2 * CUs * 64 / T): "
-                         "327 on MI355X at T=100)")
+                    help="worlds per planner per step (0: eight whole bundle waves of the device, floor(8 * CUs * 64 / T): "
+                         "1308 on MI355X at T=100; DESIGN.md section 6: 5 %% more plans/s than two waves, 327)")
     ap.add_argument("--planners", type=int, default=0,
                     help="planners per GPU planning their own batch concurrently (one HIP stream and one host thread "
                          "each): one planner's solver fills the GPU around the others'. 0 (default): 3 in weak mode "
@@ -297,7 +297,7 @@ def main():
         worlds_mine = {i: A.make_world(i, a.O, robot=geo, profile=a.profile) for i in mine}
     else:
         if a.batch <= 0:
-            a.batch = A.default_batch(a.T, local_rank)
+            a.batch = A.default_batch(a.T, local_rank, waves=8)
         mine = list(D.shard(a.batch * a.planners * world_size, rank, world_size))
 
     def setup(nplan):

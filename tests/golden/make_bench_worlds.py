@@ -2,6 +2,7 @@
 bench step plans (build container, repo root):
 
     python tests/golden/make_bench_worlds.py            # 981 worlds, ~3 min on 8 cores
+    python tests/golden/make_bench_worlds.py --extend 3924   # seeds 981..3923 (_ext.npz), ~11 min
 
 bench.py's default step at N = 1 on an MI355X (256 CUs, T = 100) is three concurrent planners x
 327 worlds = seeds 0..980 of armour_amd.make_world(seed, 20, profile="survey") (SURVEY.md §8(d)'s
@@ -57,6 +58,8 @@ def plan_one(args):
 
 def main():
     cap_study = "--cap-study" in sys.argv
+    if "--extend" in sys.argv:
+        return extend(int(sys.argv[sys.argv.index("--extend") + 1]))
     t0 = time.time()
     with mp.get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:
         out = pool.map(plan_one, [(s, 0) for s in range(N_WORLDS)], chunksize=4)
@@ -96,6 +99,34 @@ def main():
         json.dump(dict(generator="tests/golden/make_bench_worlds.py --cap-study", summary=summary, worlds=rows),
                   open(os.path.join(OUT, "bench_cap_study.json"), "w"), indent=1)
         print(json.dumps(rows, indent=1))
+
+
+def extend(total):
+    """seeds N_WORLDS .. total-1 into bench_survey_T100_O20_ext.npz: with the base fixture, the worlds
+    of bench.py's default step from round 5 on (three planners x 1308 worlds = seeds 0..3923;
+    tests/test_gpu_bench_worlds.py). The base fixture (seeds 0..980) stays what the phase-1 and
+    fidelity studies cover."""
+    t0 = time.time()
+    with mp.get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:
+        out = pool.map(plan_one, [(s, 0) for s in range(N_WORLDS, total)], chunksize=4)
+    out.sort(key=lambda t: t[0])
+    rec = dict(
+        seed=np.array([s for s, _, _ in out], dtype=np.int64),
+        digest=np.array([np.frombuffer(d, dtype=np.uint8) for _, d, _ in out]),
+        feasible=np.array([r["feasible"] for _, _, r in out]),
+        status=np.array([r["status"] for _, _, r in out], dtype=np.int32),
+        iterations=np.array([r["iterations"] for _, _, r in out], dtype=np.int32),
+        evaluations=np.array([r["evaluations"] for _, _, r in out], dtype=np.int32),
+        k_opt=np.array([r["k_opt"] for _, _, r in out]),
+        cost=np.array([r["cost"] for _, _, r in out]),
+        kkt=np.array([r["kkt"] for _, _, r in out]),
+        T=np.int64(T), O=np.int64(O),
+    )
+    np.savez_compressed(os.path.join(OUT, NAME + "_ext.npz"), **rec)
+    st = rec["status"]
+    print(json.dumps(dict(worlds=len(out), first_seed=N_WORLDS, feasible=int(rec["feasible"].sum()),
+                          converged=int((st == 0).sum()), iteration_cap=int((st == 1).sum()),
+                          local_infeasibility=int((st == 4).sum()), seconds=round(time.time() - t0, 1))), flush=True)
 
 
 if __name__ == "__main__":

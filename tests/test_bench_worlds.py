@@ -4,8 +4,9 @@ make_world(seed, 20, profile="survey") at T = 100 — with the oracle's plan of 
 
 Here: the generator still produces exactly those worlds (input digests), the oracle still
 reproduces a sample of the plans, and the fixture covers what the workload holds (feasible and
-infeasible worlds, every solver exit). tests/test_gpu_bench_worlds.py plans all 981 on the GPU in
-the bench's three concurrent batches of 327 and compares every world."""
+infeasible worlds, every solver exit). The extension (seeds 981..3923) completes bench.py's default
+step from round 5 on (three planners x 1308 worlds); tests/test_gpu_bench_worlds.py plans all 3924
+on the GPU in those three concurrent batches and compares every world."""
 import json
 import os
 
@@ -20,7 +21,15 @@ NAME = "bench_survey_T100_O20"
 
 
 def load():
+    """seeds 0..980: the phase-1 and fidelity studies' worlds"""
     return dict(np.load(os.path.join(GOLD, NAME + ".npz")))
+
+
+def load_step():
+    """the worlds of bench.py's default step: the base fixture and its extension (seeds 981..3923,
+    tests/golden/make_bench_worlds.py --extend), concatenated"""
+    a, b = load(), dict(np.load(os.path.join(GOLD, NAME + "_ext.npz")))
+    return {k: (np.concatenate([a[k], b[k]]) if np.ndim(a[k]) else a[k]) for k in a}
 
 
 def digest(world):
@@ -37,8 +46,8 @@ def bench_world(fx, i):
 
 
 def test_generator_reproduces_the_fixture_worlds():
-    fx = load()
-    assert list(fx["seed"]) == list(range(981))
+    fx = load_step()
+    assert list(fx["seed"]) == list(range(3 * 1308))
     for i in range(len(fx["seed"])):
         assert np.array_equal(digest(bench_world(fx, i)), fx["digest"][i]), f"world {i} changed"
 

@@ -1,14 +1,15 @@
 """The headline workload on the GPU against the oracle, world by world.
 
-bench.py's default step at N = 1 plans seeds 0..980 of make_world(seed, 20, profile="survey") at
-T = 100 as three concurrent planners x 327 worlds (one host thread and HIP stream each). This test
-runs exactly that step and compares every world with the oracle's plan frozen in
-tests/golden/bench_survey_T100_O20.npz (tests/golden/make_bench_worlds.py):
+bench.py's default step at N = 1 plans seeds 0..3923 of make_world(seed, 20, profile="survey") at
+T = 100 as three concurrent planners x 1308 worlds (one host thread and HIP stream each; eight whole
+bundle waves of the device per planner). This test runs exactly that step and compares every world
+with the oracle's plan frozen in tests/golden/bench_survey_T100_O20.npz and its extension _ext.npz
+(tests/golden/make_bench_worlds.py):
 
   * feasibility (finalize_solution, KPR/NLPclass.cu:422-538) and solver status identical for all
-    981 worlds;
+    3924 worlds;
   * the solver's path (iteration count, and k_opt within 1e-8 for a converged or feasible plan)
-    identical for at least 99.5 % of them; see the bar at the end. An infeasible plan writes -1
+    identical for at least 99 % of them; see the bar at the end. An infeasible plan writes -1
     (KPR/armour_main.cu:326-334), so its k_opt is not an output; its iterates run through nearly
     singular Newton systems that amplify rounding-level differences of g / J (DESIGN.md §2,
     profiles/r02_ipm_divergence.log), and it is held to identical status, iterations and
@@ -21,16 +22,16 @@ import numpy as np
 import pytest
 
 import armour_amd as A
-from test_bench_worlds import digest, load
+from test_bench_worlds import digest, load, load_step
 
 pytestmark = pytest.mark.gpu
 
 
 def test_bench_step_matches_oracle_world_by_world():
-    fx = load()
+    fx = load_step()
     T, O, W = int(fx["T"]), int(fx["O"]), len(fx["seed"])
-    batch = 327
-    assert A.default_batch(T) == batch, "the bench's default batch on this device"
+    batch = 1308
+    assert A.default_batch(T, waves=8) == batch, "the bench's default batch on this device"
     worlds = [A.make_world(int(s), O, profile="survey") for s in fx["seed"]]
     for i in (0, W // 2, W - 1):
         assert np.array_equal(digest(worlds[i]), fx["digest"][i])

@@ -69,9 +69,9 @@ for step in "$@"; do
     traffic)
       ttag=$1; batch=$2
       (cd /tmp && env "${envs[@]}" timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/${tag}_fetch" -o run -- \
-          python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 --no-extras) > "$OUT/${tag}_fetch.log" 2>&1 && \
+          python3 "$R/bench.py" --batch "$batch" --steps 1 --warmup 0 --cpu-seconds 0 --no-extras) > "$OUT/${tag}_fetch.log" 2>&1 && \
       (cd /tmp && env "${envs[@]}" timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/${tag}_write" -o run -- \
-          python3 "$R/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 --no-extras) > "$OUT/${tag}_write.log" 2>&1 && \
+          python3 "$R/bench.py" --batch "$batch" --steps 1 --warmup 0 --cpu-seconds 0 --no-extras) > "$OUT/${tag}_write.log" 2>&1 && \
       python3 tools/pmc_traffic.py "$OUT/${tag}_fetch/run_counter_collection.csv" "$OUT/${tag}_write/run_counter_collection.csv" \
           lane_reach_kernel "$OUT/${ttag}_reach_traffic.json" "$ttag" "$batch" survey
       rc=$?; [ $rc -eq 0 ] && cat "$OUT/${ttag}_reach_traffic.json" ;;

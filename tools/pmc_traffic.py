@@ -25,7 +25,7 @@ def per_dispatch(path, counter, kernel):
 def main():
     fpath, wpath, kernel, out = sys.argv[1:5]
     rnd = sys.argv[5] if len(sys.argv) > 5 else "r01"
-    batch = int(sys.argv[6]) if len(sys.argv) > 6 else 327  # bench.py's default on MI355X (256 CUs, T=100)
+    batch = int(sys.argv[6]) if len(sys.argv) > 6 else 1308  # bench.py's default on MI355X (256 CUs, T=100; 327 before round 5)
     profile = sys.argv[7] if len(sys.argv) > 7 else "default"  # world profile of the measured batch
     fetch = per_dispatch(fpath, "FETCH_SIZE", kernel)
     write = per_dispatch(wpath, "WRITE_SIZE", kernel)
@@ -37,8 +37,8 @@ def main():
                traffic_bytes_per_launch=(2 * f_kib + w_kib) * 1024,
                correction="bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md HBM)",
                config=dict(T=100, O=20, batch=batch), profile=profile, round=rnd,
-               command="rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE --output-format csv -- python3 bench.py --planners 1 "
-                       "--steps 1 --warmup 0 --cpu-seconds 0 --no-extras")
+               command=f"rocprofv3 --pmc FETCH_SIZE | --pmc WRITE_SIZE --output-format csv -- python3 bench.py --batch {batch} "
+                       "--steps 1 --warmup 0 --cpu-seconds 0 --no-extras (tools/gpu.sh traffic)")
     import hashlib
     import os
 
