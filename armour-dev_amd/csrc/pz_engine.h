@@ -577,11 +577,14 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
 // rows; views share their parent's block) to the bottom of the arena in allocation order and
 // repoint the handles; every thread of the group, at an op boundary (no operand pointer is held).
 // Owners and ranks in parallel over the MAX_SLOTS handles: a block's owner is its lowest live slot, its
-// rank the number of distinct live blocks below it (allocation order is arena order, and compaction
-// keeps it), its new offsets the sizes of the blocks ranked before it. Blocks below the first one
-// that moves stay where they are. Moves in chunks of four elements per thread: all reads of a chunk
-// before a barrier, then the writes; a block only moves down, so a chunk's writes never reach the
-// next chunk's sources.
+// rank the number of distinct live blocks below it, its new offsets the sizes of the blocks ranked
+// before it. The hash and coefficient parts are ranked separately, each by its own offset: ops of
+// different waves allocate concurrently (arena_alloc_t0 from each wave's lane 0: two atomics), so
+// two blocks' hash parts can lie in the other order than their coefficient parts, and a move in one
+// part's order would overwrite the other part's sources. Blocks below the first one that moves stay
+// where they are. Moves in chunks of four elements per thread: all reads of a chunk before a
+// barrier, then the writes; a block only moves down, so a chunk's writes never reach the next
+// chunk's sources.
 AI void arena_compact(Ctx& x, int pc) {
     Arena& A = *x.A;
     const Grp& g = x.g;
@@ -589,9 +592,14 @@ AI void arena_compact(Ctx& x, int pc) {
     long *key = tb, *shc = tb + MAX_SLOTS, *scc = tb + 2 * MAX_SLOTS;  // per slot: block hoff (-1: none), sizes
     long *boh = tb + 3 * MAX_SLOTS, *bhc = tb + 4 * MAX_SLOTS, *boc = tb + 5 * MAX_SLOTS;  // per rank
     long *bcc = tb + 6 * MAX_SLOTS, *bnh = tb + 7 * MAX_SLOTS, *bnc = tb + 8 * MAX_SLOTS;
+    long* ckey = tb + 9 * MAX_SLOTS;  // per slot: block coff (-1: none)
+#ifdef REACH_CFG_STAGE
+    static_assert(10 * MAX_SLOTS * sizeof(long) <= REACH_CFG_STAGE * sizeof(double), "compaction tables");
+#endif
     int* own = x.kp;                  // [MAX_SLOTS] owner flags (the keys are free too)
-    int* rank = x.kp + MAX_SLOTS;     // [MAX_SLOTS]
-    int* misc = x.kp + 2 * MAX_SLOTS; // block count, first block that moves
+    int* rank = x.kp + MAX_SLOTS;     // [MAX_SLOTS] hash-part rank
+    int* crank = x.kp + 2 * MAX_SLOTS;  // [MAX_SLOTS] coefficient-part rank
+    int* misc = x.kp + 3 * MAX_SLOTS; // block count, first hash / coefficient block that moves
     constexpr int B = 16;             // table reads per batch (independent loads in flight)
     static_assert(MAX_SLOTS % B == 0, "slot batches");
     const uint64_t l0 = x.live[2 * pc], l1 = x.live[2 * pc + 1];
@@ -599,10 +607,11 @@ AI void arena_compact(Ctx& x, int pc) {
     for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
         const bool lv = ((q < 64 ? l0 >> q : l1 >> (q - 64)) & 1ull) && x.H[q].cnt > 0;
         key[q] = lv ? x.H[q].hoff : -1;
+        ckey[q] = lv ? x.H[q].coff : -1;
         shc[q] = x.H[q].cnt;
         scc[q] = (long)x.H[q].cnt * x.H[q].stride;
     }
-    if (g.tid == 0) { misc[0] = 0; misc[1] = MAX_SLOTS; }
+    if (g.tid == 0) { misc[0] = 0; misc[1] = MAX_SLOTS; misc[2] = MAX_SLOTS; }
     g.sync();
     for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
         const long kq = key[q];
@@ -616,32 +625,33 @@ AI void arena_compact(Ctx& x, int pc) {
     }
     g.sync();
     for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        const long kq = key[q];
+        const long kq = key[q], cq = ckey[q];
         if (kq < 0) continue;
-        int rk = 0;
+        int rk = 0, rc = 0;
         for (int r0 = 0; r0 < MAX_SLOTS; r0 += B) {
-            long kr[B];
+            long kr[B], cr[B];
             int orr[B];
-            UNR for (int u = 0; u < B; u++) { kr[u] = key[r0 + u]; orr[u] = own[r0 + u]; }
-            UNR for (int u = 0; u < B; u++) rk += (orr[u] && kr[u] < kq) ? 1 : 0;
+            UNR for (int u = 0; u < B; u++) { kr[u] = key[r0 + u]; cr[u] = ckey[r0 + u]; orr[u] = own[r0 + u]; }
+            UNR for (int u = 0; u < B; u++) {
+                rk += (orr[u] && kr[u] < kq) ? 1 : 0;
+                rc += (orr[u] && cr[u] >= 0 && cr[u] < cq) ? 1 : 0;
+            }
         }
         rank[q] = rk;
+        crank[q] = rc;
         if (own[q]) {
             boh[rk] = kq;
             bhc[rk] = shc[q];
-            boc[rk] = x.H[q].coff;
-            bcc[rk] = scc[q];
+            boc[rc] = cq;
+            bcc[rc] = scc[q];
             int_add(&misc[0], 1);
         }
     }
     g.sync();
     const int nb = misc[0];
-    // New block offsets: a parallel prefix, each thread summing the sizes of the ranks below its own
-    // (16 independent table reads in flight). Round 4 replaced it by a one-thread loop after the
-    // LDS-arena test saw wrong offsets on the device; the cause was elsewhere (the room check in
-    // arena_ensure had no barrier behind it, so a wave could skip a compaction the others ran:
-    // DESIGN.md §4), and with that barrier the parallel and serial offsets agree bitwise on every
-    // compaction (PZ_PREFIX_CHECK=1 forms both and reports any difference).
+    // New block offsets: a parallel prefix per part, each thread summing the sizes of the ranks below
+    // its own (16 independent table reads in flight); PZ_PREFIX_CHECK=1 also forms them serially and
+    // reports any difference.
     for (int i = g.tid; i < nb; i += g.n) {
         long sh = 0, sc = 0;
         for (int r0 = 0; r0 < i; r0 += B) {
@@ -651,7 +661,8 @@ AI void arena_compact(Ctx& x, int pc) {
         }
         bnh[i] = sh;
         bnc[i] = sc;
-        if (sh != boh[i] || sc != boc[i]) int_min(&misc[1], i);
+        if (sh != boh[i]) int_min(&misc[1], i);
+        if (sc != boc[i]) int_min(&misc[2], i);
         if (i == nb - 1) {
             A.hused = sh + bhc[i];
             A.cused = sc + bcc[i];
@@ -668,25 +679,26 @@ AI void arena_compact(Ctx& x, int pc) {
 #if PZ_PREFIX_CHECK
     if (g.tid == 0) {
         long th0 = 0, tc0 = 0;
-        int fs = MAX_SLOTS;
+        int fh = MAX_SLOTS, fc = MAX_SLOTS;
         for (int r = 0; r < nb; r++) {
             if (bnh[r] != th0 || bnc[r] != tc0)
                 printf("prefix mismatch: block %d pc %d rank %d of %d: parallel (%ld, %ld) serial (%ld, %ld)\n",
                        (int)blockIdx.x, pc, r, nb, bnh[r], bnc[r], th0, tc0);
-            if ((th0 != boh[r] || tc0 != boc[r]) && r < fs) fs = r;
+            if (th0 != boh[r] && r < fh) fh = r;
+            if (tc0 != boc[r] && r < fc) fc = r;
             th0 += bhc[r];
             tc0 += bcc[r];
         }
-        if (fs != misc[1] || th0 != A.hused || tc0 != A.cused)
-            printf("prefix mismatch: block %d pc %d first %d / %d, used (%ld, %ld) / (%ld, %ld)\n", (int)blockIdx.x, pc,
-                   misc[1], fs, A.hused, A.cused, th0, tc0);
+        if (fh != misc[1] || fc != misc[2] || th0 != A.hused || tc0 != A.cused)
+            printf("prefix mismatch: block %d pc %d first %d %d / %d %d, used (%ld, %ld) / (%ld, %ld)\n", (int)blockIdx.x,
+                   pc, misc[1], misc[2], fh, fc, A.hused, A.cused, th0, tc0);
     }
     g.sync();
 #endif
-    const int first = misc[1];
+    const int first_h = misc[1], first_c = misc[2];
     const long th = A.hused, tc = A.cused;
-    if (g.tid == 0 && first < nb) A.cmoved += tc - bnc[first];
-    auto block_of = [&](const long* pre, long q) {  // the last block whose compacted start <= q
+    if (g.tid == 0 && first_c < nb) A.cmoved += tc - bnc[first_c];
+    auto block_of = [&](const long* pre, int first, long q) {  // the last block whose compacted start <= q
         int lo = first, hi = nb - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -695,13 +707,13 @@ AI void arena_compact(Ctx& x, int pc) {
         return lo;
     };
     constexpr int E = 4;
-    if (first < nb) {
-        for (long base = bnh[first]; base < th; base += (long)E * g.n) {
+    if (first_h < nb) {
+        for (long base = bnh[first_h]; base < th; base += (long)E * g.n) {
             uint64_t v[E];
             UNR for (int e = 0; e < E; e++) {
                 const long q = base + g.tid + (long)e * g.n;
                 v[e] = 0;
-                if (q < th) { const int r = block_of(bnh, q); v[e] = x.ah[boh[r] + (q - bnh[r])]; }
+                if (q < th) { const int r = block_of(bnh, first_h, q); v[e] = x.ah[boh[r] + (q - bnh[r])]; }
             }
             g.sync();
             UNR for (int e = 0; e < E; e++) {
@@ -710,12 +722,14 @@ AI void arena_compact(Ctx& x, int pc) {
             }
             g.sync();
         }
-        for (long base = bnc[first]; base < tc; base += (long)E * g.n) {
+    }
+    if (first_c < nb) {
+        for (long base = bnc[first_c]; base < tc; base += (long)E * g.n) {
             double v[E];
             UNR for (int e = 0; e < E; e++) {
                 const long q = base + g.tid + (long)e * g.n;
                 v[e] = 0;
-                if (q < tc) { const int r = block_of(bnc, q); v[e] = x.ac[boc[r] + (q - bnc[r])]; }
+                if (q < tc) { const int r = block_of(bnc, first_c, q); v[e] = x.ac[boc[r] + (q - bnc[r])]; }
             }
             g.sync();
             UNR for (int e = 0; e < E; e++) {
@@ -728,7 +742,7 @@ AI void arena_compact(Ctx& x, int pc) {
     for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
         if (key[q] < 0) continue;
         x.H[q].hoff = bnh[rank[q]];
-        x.H[q].coff = bnc[rank[q]];
+        x.H[q].coff = bnc[crank[q]];
     }
     g.sync();
 }

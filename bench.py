@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
-                    help="worlds per planner per step (0: eight whole bundle waves of the device, floor(8 * CUs * 64 / T): "
-                         "1308 on MI355X at T=100; DESIGN.md section 6: 5 %% more plans/s than two waves, 327)")
+                    help="worlds per planner per step (0: four two-wave batches, 4 * floor(2 * CUs * 64 / T), about eight "
+                         "bundle waves of the device: 1308 on MI355X at T=100; DESIGN.md section 6: 5 %% more plans/s than two waves, 327)")
     ap.add_argument("--planners", type=int, default=0,
                     help="planners per GPU planning their own batch concurrently (one HIP stream and one host thread "
                          "each): one planner's solver fills the GPU around the others'. 0 (default): 3 in weak mode "
@@ -297,7 +297,7 @@ def main():
         worlds_mine = {i: A.make_world(i, a.O, robot=geo, profile=a.profile) for i in mine}
     else:
         if a.batch <= 0:
-            a.batch = A.default_batch(a.T, local_rank, waves=8)
+            a.batch = 4 * A.default_batch(a.T, local_rank)  # 4 x 327 at T = 100: 2044 bundles, 8 waves
         mine = list(D.shard(a.batch * a.planners * world_size, rank, world_size))
 
     def setup(nplan):
