@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=0,
                     help="worlds per planner per step (0: four two-wave batches, 4 * floor(2 * CUs * 64 / T), about eight "
-                         "bundle waves of the device: 1308 on MI355X at T=100; DESIGN.md section 6: 5 %% more plans/s than two waves, 327)")
+                         "bundle waves of the device: 1308 on MI355X at T=100; one two-wave batch where T * O > 2000 "
+                         "(device memory; T=200, O=40: 163); DESIGN.md section 6: 5 %% more plans/s than two waves, 327)")
     ap.add_argument("--planners", type=int, default=0,
                     help="planners per GPU planning their own batch concurrently (one HIP stream and one host thread "
                          "each): one planner's solver fills the GPU around the others'. 0 (default): 3 in weak mode "
@@ -297,7 +298,11 @@ def main():
         worlds_mine = {i: A.make_world(i, a.O, robot=geo, profile=a.profile) for i in mine}
     else:
         if a.batch <= 0:
-            a.batch = 4 * A.default_batch(a.T, local_rank)  # 4 x 327 at T = 100: 2044 bundles, 8 waves
+            # four two-wave batches (4 x 327 at T = 100: 2044 bundles, 8 waves) where three planners'
+            # plane caches, arenas and scratch fit the device's memory with it; one where T * O is
+            # larger (config 3, T = 200 and O = 40: ~4x the per-world memory, and three planners of
+            # 4 x 163 worlds run out of device memory)
+            a.batch = (4 if a.T * a.O <= 100 * 20 else 1) * A.default_batch(a.T, local_rank)
         mine = list(D.shard(a.batch * a.planners * world_size, rank, world_size))
 
     def setup(nplan):
@@ -310,7 +315,14 @@ def main():
         else:
             si = [mine[p * a.batch:(p + 1) * a.batch] for p in range(nplan)]
             sw = [[A.make_world(i, a.O, robot=geo, profile=a.profile) for i in x] for x in si]
-        pl = [A.Planner(T=a.T, max_obstacles=a.O, max_worlds=len(x), device=local_rank, robot=robot) for x in sw]
+        pl = []
+        try:
+            for x in sw:
+                pl.append(A.Planner(T=a.T, max_obstacles=a.O, max_worlds=len(x), device=local_rank, robot=robot))
+        except BaseException:
+            for q in pl:
+                q.close()
+            raise
         return si, sw, pl
 
     P = a.planners
