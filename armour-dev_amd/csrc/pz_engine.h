@@ -585,7 +585,7 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
 // where they are. Moves in chunks of four elements per thread: all reads of a chunk before a
 // barrier, then the writes; a block only moves down, so a chunk's writes never reach the next
 // chunk's sources.
-AI void arena_compact(Ctx& x, int pc) {
+AI void arena_compact(Ctx& x, int pc, long* used_h = nullptr, long* used_c = nullptr) {
     Arena& A = *x.A;
     const Grp& g = x.g;
     long* tb = reinterpret_cast<long*>(x.stage);  // slot and block tables (the stage is free here)
@@ -697,6 +697,7 @@ AI void arena_compact(Ctx& x, int pc) {
 #endif
     const int first_h = misc[1], first_c = misc[2];
     const long th = A.hused, tc = A.cused;
+    if (used_h) { *used_h = th; *used_c = tc; }  // read by every thread before the final barrier
     if (g.tid == 0 && first_c < nb) A.cmoved += tc - bnc[first_c];
     auto block_of = [&](const long* pre, int first, long q) {  // the last block whose compacted start <= q
         int lo = first, hi = nb - 1;
@@ -747,17 +748,23 @@ AI void arena_compact(Ctx& x, int pc) {
     g.sync();
 }
 // before op pc: compact the LDS arena when fewer than nh hashes / nc coefficient rows are free
-// (every thread; the caller has synchronised, so every thread reads the same state)
-// The barrier after the reads: a thread-0 op allocates (moves hused) as soon as thread 0 passes
-// here, and a wave still reading the arena state would then decide differently (an unmatched
-// compaction barrier).
-AI void arena_ensure(Ctx& x, int pc, long nh, long nc) {
+// (every thread; the caller has synchronised, so every thread reads the same state); *used_h /
+// *used_c: the arena's use after the check, as every thread saw it.
+// late = true: the barrier after the reads. A thread-0 or wave-0 op allocates (moves hused) as soon
+// as its thread passes here, and a wave still reading the arena state would then decide differently
+// (an unmatched compaction barrier). late = false for an op that allocates only after a barrier of
+// its own (the four-wave simplify: after staging its sources).
+AI void arena_ensure(Ctx& x, int pc, long nh, long nc, long* used_h, long* used_c, bool late = true) {
     const Arena& A = *x.A;
-    if (!A.lds) return;
-    const bool room = A.hcap - A.hused >= nh && A.ccap - A.cused >= nc;
-    x.g.sync();
-    if (room) return;
-    arena_compact(x, pc);
+    const long uh = A.hused, uc = A.cused;
+    const bool room = A.hcap - uh >= nh && A.ccap - uc >= nc;
+    if (late) x.g.sync();
+    if (room) {
+        *used_h = uh;
+        *used_c = uc;
+        return;
+    }
+    arena_compact(x, pc, used_h, used_c);
 }
 
 // output header finish (thread 0): pruned amount into both independent parts (PZsparse.cu:347-349)

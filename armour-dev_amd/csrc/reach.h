@@ -507,14 +507,20 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
     }
     x.g.sync();
     int prev_sync = 1;
+    // LDS arena: free room every thread knows to be there without reading the arena state (the
+    // last check's free room less the bounds of the ops since); uniform across the group
+    long bud_h = 0, bud_c = 0;
     for (int pc = 0; pc < nops; pc++) {
         const Op op = prog[pc];
         const int par = op.par > 1 ? op.par : 1;  // ops pc .. pc + par - 1 run as one group
         if (x.A->lds) {
             // LDS arena: room for the op's output (its term count bounds the monomials it keeps),
             // compacting to the live values when short; at most half the arena is asked for, a
-            // larger output that does not fit flags ERR_ARENA (planner.hip reruns on the HBM arena)
-            if (!prev_sync) x.g.sync();
+            // larger output that does not fit flags ERR_ARENA (planner.hip reruns on the HBM arena).
+            // An op within the budget needs no check. A four-wave simplify checks without the
+            // barrier behind the reads (it allocates after its staging barrier); any other op whose
+            // bound exceeds the budget checks behind one. An op that allocates more than its bound
+            // (beyond half the arena) is caught by the allocation's capacity test (ERR_ARENA).
             long nh = 0, nc = 0;
             // (rows per output monomial: the output's element count, from the operand shapes)
             auto nel = [&](int q) { return x.H[q].R * x.H[q].C; };
@@ -536,7 +542,26 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
                     nh = 64L * par; nc = 576L * par; break;
                 default: break;
             }
-            arena_ensure(x, pc, nh < x.A->hcap / 2 ? nh : x.A->hcap / 2, nc < x.A->ccap / 2 ? nc : x.A->ccap / 2);
+            nh = nh < x.A->hcap / 2 ? nh : x.A->hcap / 2;
+            nc = nc < x.A->ccap / 2 ? nc : x.A->ccap / 2;
+            if (nh > 0 || nc > 0) {
+                const bool simp = op.code == OP_MUL || op.code == OP_ADD || op.code == OP_ADD1D ||
+                                  op.code == OP_STACK3 || op.code == OP_CROSS_PP;
+#if defined(__HIP_DEVICE_COMPILE__)
+                const bool wide = simp && (op_terms(x, op) > 64 || (x.mode & 1));  // the four-wave path
+#else
+                const bool wide = simp;
+#endif
+                if (wide || bud_h < nh || bud_c < nc) {
+                    if (!prev_sync) x.g.sync();
+                    long uh, uc;
+                    arena_ensure(x, pc, nh, nc, &uh, &uc, !wide);
+                    bud_h = x.A->hcap - uh;
+                    bud_c = x.A->ccap - uc;
+                }
+                bud_h -= nh;
+                bud_c -= nc;
+            }
         }
         prev_sync = op.sync;
 #if defined(__HIP_DEVICE_COMPILE__)
