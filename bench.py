@@ -144,16 +144,20 @@ def traffic_record(T, O, batch, profile):
     return best
 
 
-def rocprof_record(kernel="lane_reach_kernel"):
+def rocprof_record(kernel="lane_reach_kernel", solo=False):
     """The kernel's rocprofv3 --kernel-trace --stats line from the newest committed summary of the
-    same library build (profiles/r*_kernel_stats.txt written by tools/gpu.sh stats, whose header
-    names the library's SHA-1): (file, calls, average ns, min ns), or None"""
+    same library build (profiles/r*_kernel_stats*.txt written by tools/gpu.sh stats, whose header
+    names the command and the library's SHA-1): (file, calls, average ns, min ns), or None.
+    solo: a summary of `bench.py --planners 1` (every launch alone on the GPU, as the roofline's
+    `achieved` is timed); else one of the default bench (three planners)."""
     import glob
 
     digest, best = lib_digest(), None
-    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats.txt"))):
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats*.txt"))):
         lines = open(fn).read().splitlines()
         if not any(ln.startswith("# lib_sha1 ") and ln.split()[2] == digest for ln in lines):
+            continue
+        if any(ln.startswith("# stats ") and "--planners 1" in ln for ln in lines) != solo:
             continue
         for ln in lines:
             if kernel in ln and not ln.startswith("#"):
@@ -518,15 +522,19 @@ def main():
             "bytes_per_launch": lb, "frac": lb / (rk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "note": "design-independent: JRS scalars in, link and torque tables out (bench.py io_lower_bound); "
                     "the kernel's own arena traffic is the algorithmic figure above"}
-        rp = rocprof_record() if a.robot == "kinova" else None
-        if rp is not None:
-            fn, calls, avg_ns, min_ns = rp
-            line["roofline"]["rocprof"] = {
-                "source": os.path.relpath(fn, ROOT), "calls": calls, "avg_ms": avg_ns * 1e-6, "min_ms": min_ns * 1e-6,
-                "frac_avg": rk_bytes / (avg_ns * 1e-9) / 1e9 / HBM_PEAK_GBS,
-                "frac_min": rk_bytes / (min_ns * 1e-9) / 1e9 / HBM_PEAK_GBS,
-                "note": "rocprofv3 --kernel-trace --stats of this bench command on the same library build: the average "
-                        "spans the timed region's launches under three planners and the solo launch"}
+        for solo_rec, key, note in (
+                (True, "rocprof", "rocprofv3 --kernel-trace --stats of bench.py --planners 1 on the same library build: "
+                                  "every launch alone on the GPU, as `launch_ms` above"),
+                (False, "rocprof_under_load", "rocprofv3 --kernel-trace --stats of this bench command on the same library "
+                                              "build: the average spans the timed region's launches under three planners "
+                                              "and the solo launch")):
+            rp = rocprof_record(solo=solo_rec) if a.robot == "kinova" else None
+            if rp is not None:
+                fn, calls, avg_ns, min_ns = rp
+                line["roofline"][key] = {
+                    "source": os.path.relpath(fn, ROOT), "calls": calls, "avg_ms": avg_ns * 1e-6,
+                    "min_ms": min_ns * 1e-6, "frac_avg": rk_bytes / (avg_ns * 1e-9) / 1e9 / HBM_PEAK_GBS,
+                    "frac_min": rk_bytes / (min_ns * 1e-9) / 1e9 / HBM_PEAK_GBS, "note": note}
         tr = traffic_record(a.T, a.O, len(subs[0]), a.profile) if a.robot == "kinova" else None
         if tr is not None:
             line["roofline"]["traffic"] = tr[1]["traffic_bytes_per_launch"]
