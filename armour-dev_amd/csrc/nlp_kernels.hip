@@ -312,6 +312,23 @@ __device__ void extremum(int kind, double q0, double Tqd0, double TTqdd0, double
     *e2o = e2;
     *e3o = e3;
 }
+// EVAL_PROF=1 (diagnostic builds only: make lane_variant LW=4 LX=_evprof EXTRA=-DEVAL_PROF=1): thread 0
+// of blocks (t = 0 | 50, list entry 0) prints its phase boundaries (wall clock, 10 ns ticks)
+#ifndef EVAL_PROF
+#define EVAL_PROF 0
+#endif
+#define EVP_DECL unsigned long long evp_[10]; int evn_ = 0;
+#define EVP_MARK if (EVAL_PROF && threadIdx.x == 0 && evn_ < 10) evp_[evn_++] = wall_clock64();
+#define EVP_PRINT(tag)                                                                                   \
+    if (EVAL_PROF && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 50) && blockIdx.y == 0) {      \
+        EVP_MARK                                                                                           \
+        printf("%s t=%d grid=%d n=%d: %llu %llu %llu %llu %llu %llu %llu %llu %llu\n", tag, (int)blockIdx.x,    \
+               (int)gridDim.y, evn_, evn_ > 1 ? evp_[1] - evp_[0] : 0ull, evn_ > 2 ? evp_[2] - evp_[1] : 0ull,      \
+               evn_ > 3 ? evp_[3] - evp_[2] : 0ull, evn_ > 4 ? evp_[4] - evp_[3] : 0ull,                         \
+               evn_ > 5 ? evp_[5] - evp_[4] : 0ull, evn_ > 6 ? evp_[6] - evp_[5] : 0ull,                         \
+               evn_ > 7 ? evp_[7] - evp_[6] : 0ull, evn_ > 8 ? evp_[8] - evp_[7] : 0ull,                         \
+               evn_ > 9 ? evp_[9] - evp_[8] : 0ull);                                                             \
+    }
 __device__ double extremum_grad(int kind, int id, double e2, double e3) {
     // envelope theorem: d/dk of the value at an interior critical point (oracle/src/traj.cpp)
     if (id == 1) return 0.0;
@@ -662,6 +679,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
     // (restoration launches, d.resto: the worlds in the restoration phase, WS_RESTO)
     if (mode == 1 && !((d.resto ? S.status == WS_RESTO : S.status == 0) && S.searching)) return;
     if (mode == 5 && !(d.resto ? (S.status == WS_RESTO && S.rpend) : (S.status == 0 && S.spec_k >= 0))) return;
+    EVP_DECL EVP_MARK
     const int slot = mode == 0 ? 0 : 1 - S.cur;
     double* const Gb = d.g + gidx(d, slot, w, 0);
     double* const Jb = d.J + gidx(d, slot, w, 0) * NF;
@@ -713,6 +731,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
         for (int i = tid; i < O * 12; i += blockDim.x) obs[i / 12][i % 12] = d.obs[(long)w * O * 12 + i];
     }
     __syncthreads();
+    EVP_MARK
     if (!(d.diag & 1)) {
         // only the valid monomials, enumerated compactly (one load round per thread): u < L are
         // link monomials, the rest torque monomials; prefix offsets from the per-PZ counts
@@ -748,6 +767,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
         }
     }
     __syncthreads();
+    EVP_MARK
     // slices (PZsparse.cu:404-435 value, :477-516 gradient): one thread per output — k = 0 the
     // value, k = 1..7 the derivative in x_{k-1} — summing its terms in monomial order. Powers come
     // from a per-variable table (ptab, filled with the staging), x_j^g as the reference forms it.
@@ -858,6 +878,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
         }
     }
     __syncthreads();
+    EVP_MARK
     // collision rows (CollisionChecking.cu:230-299). Of the 36 planes of a buffered obstacle, the
     // 15 spanned by two link generators do not depend on the obstacle and the 3 spanned by two
     // obstacle generators do not depend on the link: those are formed once per block, with the
@@ -905,6 +926,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
                 pidx[pr] = 0xFFFFFFFFu;
             }
             __syncthreads();
+            EVP_MARK
             auto cand = [&](int q, double& v, int& sub, int& pr, double* a) {
                 a[0] = rec[q];
                 a[1] = rec[cap + q];
@@ -933,12 +955,14 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
                     }
                 }
                 __syncthreads();
+                EVP_MARK
 #pragma unroll
                 for (int s = 0; s < RPT; s++) {
                     const int q = tid + s * EVAL_THREADS;
                     if (q < total && v[s] > start && v[s] == dkey(pkey[pq[s]])) atomicMin(&pidx[pq[s]], (unsigned)(2 * q + sub[s]));
                 }
                 __syncthreads();
+                EVP_MARK
 #pragma unroll
                 for (int s = 0; s < RPT; s++) {
                     const int q = tid + s * EVAL_THREADS;
@@ -955,6 +979,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
                     if (v > start) atomicMax(&pkey[pr], okey(v));
                 }
                 __syncthreads();
+                EVP_MARK
                 for (int q = tid; q < total; q += blockDim.x) {
                     double v, a[3];
                     int sub, pr;
@@ -962,6 +987,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
                     if (v > start && v == dkey(pkey[pr])) atomicMin(&pidx[pr], (unsigned)(2 * q + sub));
                 }
                 __syncthreads();
+                EVP_MARK
                 for (int q = tid; q < total; q += blockDim.x) {
                     double v, a[3];
                     int sub, pr;
@@ -973,6 +999,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
                 }
             }
             __syncthreads();
+            EVP_MARK
             for (int pr = tid; pr < NP; pr += blockDim.x) {
                 const int l = pr / O, o = pr % O;
                 const unsigned wi = pidx[pr];
@@ -1056,6 +1083,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
         mixc[u] = (int8_t)code;
     }
     __syncthreads();
+    EVP_MARK
     // one thread per (link, obstacle) completes the 36-plane scan in the reference's order (pairs
     // (a, b), a < b, lexicographic: CollisionChecking.cu:26-39; pos_p before neg_p, strict >), so the
     // first maximum wins as in the reference's serial loop; a mixed run (a < 3 <= b) enters as its
@@ -1129,6 +1157,7 @@ __device__ __attribute__((always_inline)) void eval_body(const NlpDev& d, int mo
         }
     }
     }
+    EVP_PRINT("EV")
 }
 
 // the product evaluation is fp64; eval_kernel_t<float> serves only the fp32 tolerance study
@@ -1167,6 +1196,7 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     const WorldState& S = d.ws[w];
     // (restoration launches, d.resto: the trials of the phase's Armijo search)
     if (!(d.resto ? (S.status == WS_RESTO && S.searching) : (S.status == 0 && (d.b_in_cs || S.searching)))) return;
+    EVP_DECL EVP_MARK
     const RobotParams& rp = *d.rp;
     const int tid = threadIdx.x, K = d.K;
     const long jt = (long)w * d.T + t;
@@ -1193,6 +1223,7 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     if (tid >= 64 && tid < 64 + NJ) lcnt[tid - 64] = d.ro.link_cnt[jt * NJ + tid - 64];
     if (tid >= 96 && tid < 96 + NF) tcnt[tid - 96] = d.nt ? d.ro.tq_cnt[jt * NF + tid - 96] : 0;
     __syncthreads();
+    EVP_MARK
     {
         int lpre[MAX_J + 1], tpre[NF + 1];
         lpre[0] = 0;
@@ -1226,6 +1257,7 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
         }
     }
     __syncthreads();
+    EVP_MARK
     // value slices of every trial: link centres (k, l, e) and torque rows (k, j), monomial order
     auto vterm = [&](double co, int h, int kk) {
         double v = co;
@@ -1265,26 +1297,31 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
             d.gs[((long)i * K + kk) * d.m + (long)t * NF + j] = ((c - r) + (c + r)) * 0.5;
         }
     }
-    if (t == 0 && tid >= (int)blockDim.x - K) {
-        // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267) of trial kk
+    // extremum rows (NLPclass.cu:319-320, 390-391) and cost (NLPclass.cu:207-267) of every trial:
+    // task v = (kind, joint) for v < 2 NF, the cost for v = 2 NF, on blocks t = v (mod T), one lane
+    // per trial in the last wave. Each extremum is a chain of dependent fp64 divisions and roots
+    // (~0.8 us); spread over blocks, no block's critical path holds more than one (all on block 0
+    // they were 14 in a row, about half the launch in the solver's tail).
+    for (int v = t; v <= 2 * NF && tid >= (int)blockDim.x - K; v += d.T) {
         const int kk = tid - ((int)blockDim.x - K);
         const double* x = xk[kk];
         double* const Gb = d.gs + ((long)i * K + kk) * d.m;
-        const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
         const double* q0 = d.q0 + w * NF;
         const double* qd0 = d.qd0 + w * NF;
         const double* qdd0 = d.qdd0 + w * NF;
         const double D = rp.duration;
-        for (int kind = 0; kind < 2; kind++)
-            for (int j = 0; j < NF; j++) {
-                double mn, mx, e2, e3;
-                int mnid, mxid;
-                extremum(kind, q0[j], qd0[j] * D, qdd0[j] * D * D, rp.k_range[j] * x[j], &mn, &mx, &mnid, &mxid, &e2, &e3);
-                const double scale = kind == 0 ? 1.0 : D;
-                const long rmin = off2 + kind * 2 * NF + j;
-                Gb[rmin] = mn / scale;
-                Gb[rmin + NF] = mx / scale;
-            }
+        if (v < 2 * NF) {
+            const long off2 = (long)NF * d.T + (long)d.T * d.NJ * d.O;
+            const int kind = v / NF, j = v % NF;
+            double mn, mx, e2, e3;
+            int mnid, mxid;
+            extremum(kind, q0[j], qd0[j] * D, qdd0[j] * D * D, rp.k_range[j] * x[j], &mn, &mx, &mnid, &mxid, &e2, &e3);
+            const double scale = kind == 0 ? 1.0 : D;
+            const long rmin = off2 + kind * 2 * NF + j;
+            Gb[rmin] = mn / scale;
+            Gb[rmin + NF] = mx / scale;
+            continue;
+        }
         const double tp = rp.t_plan;
         double qp[NF];
         for (int j = 0; j < NF; j++) qp[j] = bz_q(q0[j], qd0[j] * D, qdd0[j] * D * D, rp.k_range[j] * x[j], tp);
@@ -1301,10 +1338,14 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
         d.fs[(long)i * K + kk] = fv * rp.cost_scale;
     }
     __syncthreads();
+    EVP_MARK
     // collision rows of every trial from the plane cache, record-parallel as eval_kernel_t's scan:
     // every thread takes records straight from global memory and forms each trial's two candidates;
     // the (trial, pair) maximum by an LDS atomicMax on an order-preserving key (the value is all a
     // trial needs; a +-0 tie cannot change the line search's terms). Tables in the slicing buffer.
+    // (Measured slower: one thread per pair scanning its records, 2x in the solver's tail: a pair's
+    // records are a dependent chain of loads on one lane; and each thread reducing four consecutive
+    // records before its atomics, strided loads.)
     const unsigned last = NP > 0 ? d.pcoff[jt * NP + NP - 1] : 0u;
     const int total = (int)(last >> 8) + (int)(last & 255);
     const unsigned long long pb = d.pcbase[jt];
@@ -1316,6 +1357,7 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
     const double start = -100000000.0;
     for (int u = tid; u < K * NP; u += blockDim.x) pkey[u] = okey(start);
     __syncthreads();
+    EVP_MARK
     for (int q = tid; q < total; q += blockDim.x) {
         const double a0 = rec[q], a1 = rec[cap + q], a2 = rec[2 * cap + q];
         const double P = rec[3 * cap + q], N = rec[4 * cap + q];
@@ -1328,11 +1370,13 @@ __device__ __attribute__((always_inline)) void eval_trials_body(const NlpDev& d)
         }
     }
     __syncthreads();
+    EVP_MARK
     for (int u = tid; u < K * NP; u += blockDim.x) {
         const int kk = u / NP, pr = u - kk * NP;
         const int l = pr / O, o = pr % O;
         d.gs[((long)i * K + kk) * d.m + nt + ((long)l * d.T + t) * O + o] = -dkey(pkey[u]);
     }
+    EVP_PRINT("TR")
 }
 __global__ __launch_bounds__(EVAL_THREADS) void eval_trials_kernel(NlpDev d) { eval_trials_body<CAP_LM, CAP_UM, UB_FULL>(d); }
 // the sync-free tail's single line-search round: all max_ls trials (K = EV_MAXK + 1) of the few
