@@ -107,6 +107,8 @@ struct Ctx {
     double thr;
     unsigned long long* phase;  // optional large-operator phase cycle counters [8] (profiling)
     int mode;          // diagnostics: bit 0 = no wave-0 path
+    int pc;            // LDS arena: the op being run (its live mask, for a compaction inside it)
+    long bud_h, bud_c; // LDS arena: room every thread knows to be free (run_program)
 };
 
 enum : int { ERR_ARENA = 1, ERR_SORTCAP = 2, ERR_LINKGEN = 4, ERR_OUTCAP = 8, ERR_HANDLES = 16 };
@@ -594,12 +596,15 @@ AI void arena_compact(Ctx& x, int pc, long* used_h = nullptr, long* used_c = nul
     long *bcc = tb + 6 * MAX_SLOTS, *bnh = tb + 7 * MAX_SLOTS, *bnc = tb + 8 * MAX_SLOTS;
     long* ckey = tb + 9 * MAX_SLOTS;  // per slot: block coff (-1: none)
 #ifdef REACH_CFG_STAGE
-    static_assert(10 * MAX_SLOTS * sizeof(long) <= REACH_CFG_STAGE * sizeof(double), "compaction tables");
+    static_assert(10 * MAX_SLOTS * sizeof(long) + (3 * MAX_SLOTS + 3) * sizeof(int) <= REACH_CFG_STAGE * sizeof(double),
+                  "compaction tables");
 #endif
-    int* own = x.kp;                  // [MAX_SLOTS] owner flags (the keys are free too)
-    int* rank = x.kp + MAX_SLOTS;     // [MAX_SLOTS] hash-part rank
-    int* crank = x.kp + 2 * MAX_SLOTS;  // [MAX_SLOTS] coefficient-part rank
-    int* misc = x.kp + 3 * MAX_SLOTS; // block count, first hash / coefficient block that moves
+    // the int tables after the long ones, also in the stage: a compaction inside a simplify (after
+    // its key scan) must leave the op's keys and positions (x.kh / x.ki / x.kp) alone
+    int* own = reinterpret_cast<int*>(tb + 10 * MAX_SLOTS);  // [MAX_SLOTS] owner flags
+    int* rank = own + MAX_SLOTS;      // [MAX_SLOTS] hash-part rank
+    int* crank = own + 2 * MAX_SLOTS; // [MAX_SLOTS] coefficient-part rank
+    int* misc = own + 3 * MAX_SLOTS;  // block count, first hash / coefficient block that moves
     constexpr int B = 16;             // table reads per batch (independent loads in flight)
     static_assert(MAX_SLOTS % B == 0, "slot batches");
     const uint64_t l0 = x.live[2 * pc], l1 = x.live[2 * pc + 1];
@@ -749,16 +754,14 @@ AI void arena_compact(Ctx& x, int pc, long* used_h = nullptr, long* used_c = nul
 }
 // before op pc: compact the LDS arena when fewer than nh hashes / nc coefficient rows are free
 // (every thread; the caller has synchronised, so every thread reads the same state); *used_h /
-// *used_c: the arena's use after the check, as every thread saw it.
-// late = true: the barrier after the reads. A thread-0 or wave-0 op allocates (moves hused) as soon
-// as its thread passes here, and a wave still reading the arena state would then decide differently
-// (an unmatched compaction barrier). late = false for an op that allocates only after a barrier of
-// its own (the four-wave simplify: after staging its sources).
-AI void arena_ensure(Ctx& x, int pc, long nh, long nc, long* used_h, long* used_c, bool late = true) {
+// *used_c: the arena's use after the check, as every thread saw it. The barrier after the reads: a
+// thread-0 or wave-0 op allocates (moves hused) as soon as its thread passes here, and a wave still
+// reading the arena state would then decide differently (an unmatched compaction barrier).
+AI void arena_ensure(Ctx& x, int pc, long nh, long nc, long* used_h, long* used_c) {
     const Arena& A = *x.A;
     const long uh = A.hused, uc = A.cused;
     const bool room = A.hcap - uh >= nh && A.ccap - uc >= nc;
-    if (late) x.g.sync();
+    x.g.sync();
     if (room) {
         *used_h = uh;
         *used_c = uc;
@@ -1063,7 +1066,9 @@ AI bool order_keys(Ctx& x, const Terms& T, int N, KeyBufs& K) {
 #endif
 
 // group sums in term order, keep flags and pruned amounts, compaction, output (keys ordered)
-template <class Pol>
+// LA: the build can run on the LDS arena (reach_kernel<NT, true>, the host emulation); the HBM
+// kernels compile without its exact-size check (its inlined compaction would cost them registers)
+template <class Pol, bool LA = true>
 AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, const KeyBufs& K) {
     const Grp& g = x.g;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1094,8 +1099,19 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
         kp[q] = keep;
     }
     g.sync();
+    // LDS arena: the room this output needs is known exactly once the keeps are counted. The arena
+    // state is read here, before the scan's barriers: nothing allocates until thread 0 does below.
+    // Pass 2 reads only the keys, the positions and the parked sums, not the sources, so the
+    // arena can be compacted after the scan (arena_compact keeps its tables in the stage).
+    long uh = 0, uc = 0;
+    if (LA && x.A->lds) { uh = x.A->hused; uc = x.A->cused; }
     PHASE(2)
     const int K_ = block_scan(x, kp, N);
+    if (LA && x.A->lds) {
+        if (!(x.A->hcap - uh >= K_ && x.A->ccap - uc >= (long)K_ * n)) arena_compact(x, x.pc, &uh, &uc);
+        x.bud_h = x.A->hcap - uh - K_;
+        x.bud_c = x.A->ccap - uc - (long)K_ * n;
+    }
     if (g.tid == 0) {
         arena_alloc_t0(x, x.H[o], K_, n);
         x.A->bytes += T.in_bytes() + (double)K_ * (8.0 + 8.0 * n);

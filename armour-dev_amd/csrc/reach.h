@@ -487,6 +487,7 @@ inline int* g_op_stats = nullptr;
 // host emulation: per op, the output handle's monomial hashes (structure studies)
 inline void (*g_hash_sink)(int pc, const uint64_t* h, int n) = nullptr;
 #endif
+template <bool LA = true>  // LA: may run on the LDS arena (see simplify_groups)
 AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int T, int t, const double* q0,
                     const double* qd0, const double* qdd0, const ReachOut& out, long j, JrsJoint* jrs,
                     double* scratch, unsigned long long* prof, double* dump = nullptr, const JrsJoint* jrs_in = nullptr) {
@@ -509,18 +510,21 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
     int prev_sync = 1;
     // LDS arena: free room every thread knows to be there without reading the arena state (the
     // last check's free room less the bounds of the ops since); uniform across the group
-    long bud_h = 0, bud_c = 0;
+    x.bud_h = 0;
+    x.bud_c = 0;
     for (int pc = 0; pc < nops; pc++) {
         const Op op = prog[pc];
         const int par = op.par > 1 ? op.par : 1;  // ops pc .. pc + par - 1 run as one group
-        if (x.A->lds) {
+        x.pc = pc;
+        if (LA && x.A->lds) {
             // LDS arena: room for the op's output (its term count bounds the monomials it keeps),
             // compacting to the live values when short; at most half the arena is asked for, a
             // larger output that does not fit flags ERR_ARENA (planner.hip reruns on the HBM arena).
-            // An op within the budget needs no check. A four-wave simplify checks without the
-            // barrier behind the reads (it allocates after its staging barrier); any other op whose
-            // bound exceeds the budget checks behind one. An op that allocates more than its bound
-            // (beyond half the arena) is caught by the allocation's capacity test (ERR_ARENA).
+            // An op within the budget needs no check. A four-wave simplify checks its exact need
+            // itself, after counting its keeps (simplify_groups), and sets the budget; any other op
+            // whose bound exceeds the budget checks behind a barrier. An op that allocates more
+            // than its bound (beyond half the arena) is caught by the allocation's capacity test
+            // (ERR_ARENA).
             long nh = 0, nc = 0;
             // (rows per output monomial: the output's element count, from the operand shapes)
             auto nel = [&](int q) { return x.H[q].R * x.H[q].C; };
@@ -552,15 +556,17 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 #else
                 const bool wide = simp;
 #endif
-                if (wide || bud_h < nh || bud_c < nc) {
-                    if (!prev_sync) x.g.sync();
-                    long uh, uc;
-                    arena_ensure(x, pc, nh, nc, &uh, &uc, !wide);
-                    bud_h = x.A->hcap - uh;
-                    bud_c = x.A->ccap - uc;
+                if (!wide) {
+                    if (x.bud_h < nh || x.bud_c < nc) {
+                        if (!prev_sync) x.g.sync();
+                        long uh, uc;
+                        arena_ensure(x, pc, nh, nc, &uh, &uc);
+                        x.bud_h = x.A->hcap - uh;
+                        x.bud_c = x.A->ccap - uc;
+                    }
+                    x.bud_h -= nh;
+                    x.bud_c -= nc;
                 }
-                bud_h -= nh;
-                bud_c -= nc;
             }
         }
         prev_sync = op.sync;
@@ -691,10 +697,10 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 #if defined(__HIP_DEVICE_COMPILE__)
                 if (x.phase && tid == 0) x.phase[1] += (unsigned long long)(clock64() - pt);
 #endif
-                if (cls == 0) simplify_groups(x, op.o, Tm, p1, N, K);
-                else if (cls == 1) simplify_groups(x, op.o, Tm, p3, N, K);
-                else if (cls == 2) simplify_groups(x, op.o, Tm, p9, N, K);
-                else simplify_groups(x, op.o, Tm, pp, N, K);
+                if (cls == 0) simplify_groups<decltype(p1), LA>(x, op.o, Tm, p1, N, K);
+                else if (cls == 1) simplify_groups<decltype(p3), LA>(x, op.o, Tm, p3, N, K);
+                else if (cls == 2) simplify_groups<decltype(p9), LA>(x, op.o, Tm, p9, N, K);
+                else simplify_groups<decltype(pp), LA>(x, op.o, Tm, pp, N, K);
                 break;
             }
         }

@@ -238,7 +238,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
             qdd0s[threadIdx.x] = a.qdd0[w * NF + threadIdx.x];
         }
         __syncthreads();
-        run_program(x, rp, a.prog, a.nops, a.T, t, q0s, qd0s, qdd0s, out, job, jrs, scratch, a.prof,
+        run_program<LA>(x, rp, a.prog, a.nops, a.T, t, q0s, qd0s, qdd0s, out, job, jrs, scratch, a.prof,
                     job == 0 ? a.dump : nullptr, a.jrs + job * NF);
         if (threadIdx.x == 0) {
             if (err) atomicOr(&out.err[w], err);
