@@ -587,7 +587,7 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
 // where they are. Moves in chunks of four elements per thread: all reads of a chunk before a
 // barrier, then the writes; a block only moves down, so a chunk's writes never reach the next
 // chunk's sources.
-AI void arena_compact(Ctx& x, int pc, long* used_h = nullptr, long* used_c = nullptr) {
+__device__ __host__ __attribute__((noinline)) void arena_compact(Ctx& x, int pc, long* used_h = nullptr, long* used_c = nullptr) {
     Arena& A = *x.A;
     const Grp& g = x.g;
     long* tb = reinterpret_cast<long*>(x.stage);  // slot and block tables (the stage is free here)
