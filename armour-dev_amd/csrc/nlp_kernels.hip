@@ -184,11 +184,14 @@ __device__ inline __attribute__((always_inline)) void mixed_plane(const R* ga, c
 template <typename R>
 __device__ inline __attribute__((always_inline)) void mixed_plane_j(int j, const R* ga, const R (*G)[3], const R* oc,
                                                                     R* C, R& dd, R& del) {
+    // every case indexes G with a constant: a run-time row index would place a private G in scratch
     switch (j) {
+        case 0: mixed_plane<-1>(ga, G[OBS_GEN + 0], G, oc, C, dd, del); break;
+        case 1: mixed_plane<-1>(ga, G[OBS_GEN + 1], G, oc, C, dd, del); break;
+        case 2: mixed_plane<-1>(ga, G[OBS_GEN + 2], G, oc, C, dd, del); break;
         case 3: mixed_plane<0>(ga, G[OBS_GEN + 3], G, oc, C, dd, del); break;
         case 4: mixed_plane<1>(ga, G[OBS_GEN + 4], G, oc, C, dd, del); break;
-        case 5: mixed_plane<2>(ga, G[OBS_GEN + 5], G, oc, C, dd, del); break;
-        default: mixed_plane<-1>(ga, G[OBS_GEN + j], G, oc, C, dd, del); break;
+        default: mixed_plane<2>(ga, G[OBS_GEN + 5], G, oc, C, dd, del); break;
     }
 }
 
@@ -506,10 +509,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
         double G[BUF_GEN][3], oc[3];
         load_gens(l, o, G, oc);
         double M = -1e300;
+        const double* const ga = obs[o] + 3 * (i + 1);  // G[i], read from LDS (a run-time row of G would be scratch)
 #pragma unroll
         for (int j = 0; j < 6; j++) {
             double A[3], dd, del, lo, hi;
-            mixed_plane_j(j, G[i], G, oc, A, dd, del);
+            mixed_plane_j(j, ga, G, oc, A, dd, del);
             pc_bounds(A, dd + del, -dd + del, cen[l], rad[l], lo, hi);
             if (nonzero3(A)) M = fmax(M, lo);
         }
@@ -545,10 +549,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
         load_gens(l, o, G, oc);
         const double M = pairM[u / OBS_GEN] - PC_MARGIN;
         unsigned bits = 0;
+        const double* const ga = obs[o] + 3 * (i + 1);
 #pragma unroll
         for (int j = 0; j < 6; j++) {
             double A[3], dd, del, lo, hi;
-            mixed_plane_j(j, G[i], G, oc, A, dd, del);
+            mixed_plane_j(j, ga, G, oc, A, dd, del);
             pc_bounds(A, dd + del, -dd + del, cen[l], rad[l], lo, hi);
             if (nonzero3(A) && hi >= M) bits |= 1u << j;
         }
@@ -630,7 +635,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void plane_cache_kernel(NlpDev d) {
                 if (!((bits >> pos++) & 1ull)) continue;
                 double A[3], dd, del;
                 if (a < OBS_GEN && b >= OBS_GEN) {
-                    mixed_plane_j(b - OBS_GEN, G[a], G, oc, A, dd, del);
+                    mixed_plane_j(b - OBS_GEN, obs[o] + 3 * (a + 1), G, oc, A, dd, del);
                 } else {
                     const double* P = b < OBS_GEN ? oop[o][a + b - 1] : llp[l][(a - OBS_GEN) * (11 - (a - OBS_GEN)) / 2 + b - a - 1];
                     A[0] = P[0]; A[1] = P[1]; A[2] = P[2];
