@@ -239,3 +239,22 @@ def test_lds_arena_matches_hbm_arena(scale):
             assert np.array_equal(lds.torque_radius(0), base.torque_radius(0))
             assert np.array_equal(lds.constraints(0), base.constraints(0))
             assert np.array_equal(lds.link_centers(0), base.link_centers(0))
+
+
+@pytest.mark.parametrize("T", [10, 14])
+def test_short_horizon_plans_match_oracle(T):
+    """Horizons shorter than the 2 NF + 1 = 15 extremum / cost tasks of a trial evaluation: the
+    trial kernel (eval_trials_body) spreads them over blocks t = v (mod T), so some blocks take two.
+    A batch (the speculative trial path) and single-world plans against the oracle's plans."""
+    O = 3
+    worlds = [A.make_world(900 + s, O) for s in range(6)]
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds))
+    res, _ = P.plan(worlds)
+    for w, r in enumerate(res):
+        ro = OraclePlanner(*worlds[w], T=T, threads=4).plan()
+        assert r["error"] == 0
+        assert (r["feasible"], r["status"]) == (ro["feasible"], ro["status"]), (w, r["status"], ro["status"])
+        it_tol = 5 if (r["status"] == 4 and not r["feasible"]) else 0
+        assert abs(r["iterations"] - ro["iterations"]) <= it_tol, (w, r["iterations"], ro["iterations"])
+        if r["status"] == 0 or r["feasible"]:
+            np.testing.assert_allclose(r["k_opt"], ro["k_opt"], rtol=0, atol=1e-8)
