@@ -187,17 +187,34 @@ int plan_dir(const Lib& L, armour_planner* served, const std::string& dir, int c
     // a fresh armour.out on every run, as the reference (armour_main.cu:36-37); a served request's
     // client truncated it already (a server must not touch the file of a client that gave up)
     if (client < 0) { std::ofstream o(out1); }
+    // served: the .part files written so far are removed on every return that does not commit
+    // them, and a failure writes its -1 under the directory lock only while the client waits (the
+    // commit protocol below), so a late failure never touches a directory its client left
+    std::vector<std::string> parts;
+    struct PartSweep {
+        std::vector<std::string>& parts;
+        ~PartSweep() {
+            for (const auto& f : parts) std::remove((f + ".part").c_str());
+        }
+    } sweep{parts};
+    auto fail = [&](const char* msg) {
+        if (client < 0) return fail_out(out1, msg);
+        DirLock lk(dir);
+        if (peer_waiting(client)) return fail_out(out1, msg);
+        std::fprintf(stderr, "armour_main --serve: client of %s gave up; failure (%s) discarded\n", dir.c_str(), msg);
+        return 1;
+    };
 
     double q0[NF], qd0[NF], qdd0[NF], qdes[NF];
     int O = 0;
     std::vector<double> obs;
     {
         std::ifstream is(in);
-        if (!is.is_open()) return fail_out(out1, "error reading input file");
+        if (!is.is_open()) return fail("error reading input file");
         for (double* v : {q0, qd0, qdd0, qdes})
             for (int i = 0; i < NF; i++) is >> v[i];
         is >> O;
-        if (O > MAX_OBSTACLES || O < 0) return fail_out(out1, "number of obstacles larger than MAX_OBSTACLE_NUM");
+        if (O > MAX_OBSTACLES || O < 0) return fail("number of obstacles larger than MAX_OBSTACLE_NUM");
         obs.assign((size_t)O * ARMOUR_OBSTACLE_DOUBLES, 0.0);
         for (double& v : obs) is >> v;
     }
@@ -207,7 +224,7 @@ int plan_dir(const Lib& L, armour_planner* served, const std::string& dir, int c
     if (!p) {
         armour_config cfg{0, T, O, 1, 0, 0};
         p = L.create(&cfg);
-        if (!p) return fail_out(out1, L.last_error());
+        if (!p) return fail(L.last_error());
     }
     struct Owned {
         const Lib& L;
@@ -231,7 +248,7 @@ int plan_dir(const Lib& L, armour_planner* served, const std::string& dir, int c
     po.link_centers = centers.data();
     po.link_generators = gens.data();
     po.torque_radius = rad.data();
-    if (L.plan(p, &w, &po) != 0) return fail_out(out1, L.last_error());
+    if (L.plan(p, &w, &po) != 0) return fail(L.last_error());
     const armour_result& r = po.result;
     const armour_timing& tm = po.timing;
     std::cout << "        HIP: reachable sets " << tm.reach_ms << " ms, solver " << tm.nlp_ms << " ms, "
@@ -243,8 +260,7 @@ int plan_dir(const Lib& L, armour_planner* served, const std::string& dir, int c
     // the reference's writers are ofstreams at setprecision(10) / (6) (armour_main.cu:319-398),
     // i.e. printf's %.10g / %.6g; std::to_chars(general, precision) is specified as exactly that
     // conversion and is several times faster for the ~40k numbers a T = 128 plan writes
-    std::vector<std::string> parts;  // served: the .part files to commit
-    auto dst = [&](const std::string& name) {
+    auto dst = [&](const std::string& name) {  // served: the .part files to commit (`parts`)
         if (client < 0) return dir + name;
         parts.push_back(dir + name);
         return dir + name + ".part";
@@ -285,6 +301,7 @@ int plan_dir(const Lib& L, armour_planner* served, const std::string& dir, int c
             const std::string tmp = f + ".part";
             if (!keep || std::rename(tmp.c_str(), f.c_str()) != 0) std::remove(tmp.c_str());
         }
+        parts.clear();
         if (!keep) {
             std::fprintf(stderr, "armour_main --serve: client of %s gave up; plan discarded\n", dir.c_str());
             return 1;

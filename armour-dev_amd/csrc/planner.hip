@@ -476,12 +476,16 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // active-world lists: two per iteration (ping-pong), two per line-search round
     // (+ two for the restoration phases inside the interior-point loop)
     if ((rc = p->alloc(&p->d_lists, 6 * (size_t)Wm)) || (rc = p->alloc(&d.cnt, 16))) return rc;
-    // certified plane cache: a region of PC_K records per (link, obstacle) pair for every (world, t)
-    // (ARMOUR_PC_K, 1..36). The survey workload keeps 5.3 planes per pair on average; a (world, t)
-    // whose kept planes exceed its region is flagged (pcok) and evaluated by the full scan, with
-    // bitwise the same results, so the region size trades memory for speed only. Round 4 reserved
-    // all 36 (42 MB per world at T = 100, O = 20), which capped the batch a GPU can hold.
-    d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0);
+    // certified plane cache: one record pool sized for PC_K records per (link, obstacle) pair of
+    // every (world, t) (ARMOUR_PC_K, 1..36); each (world, t) block takes its records from the pool
+    // with one atomic (pcbase). The survey workload keeps 5.3 planes per pair on average. A build
+    // that needs more than the pool is repeated on a larger pool (ensure_plane_cache); if that pool
+    // cannot be allocated, the cache is not marked ready and the solve runs on the full scan
+    // (bitwise the same results, slower). Round 4 reserved all 36 per pair (42 MB per world at
+    // T = 100, O = 20), which capped the batch a GPU can hold. The pool counter is 32-bit: a batch
+    // whose 36 records per pair could exceed it does not use the cache.
+    d.pcache = !(std::getenv("ARMOUR_PLANE_CACHE") && std::atoi(std::getenv("ARMOUR_PLANE_CACHE")) == 0) &&
+               (double)COMB * NJ * std::max(Om, 1) * (double)jobs < 4294967295.0;
     d.pcready = 0;
     {
         const char* pk = std::getenv("ARMOUR_PC_K");
@@ -778,18 +782,28 @@ static void ensure_plane_cache(armour_planner* p) {
     // The pool is sized at creation for ARMOUR_PC_K records per pair; a build whose blocks need
     // more (the count is known only on the device) is repeated on a pool of 1.25x what it needed,
     // so every block is cached. One host wait on the build, which the solver's first kernels wait
-    // for anyway.
-    for (int attempt = 0; attempt < 2; attempt++) {
+    // for anyway. The cache is marked ready only when the last build fitted its pool: the cached
+    // kernels read every block's records from its pool offset, and a block that did not fit has
+    // none there. Otherwise (the larger pool cannot be allocated) this solve runs on the full
+    // 36-plane scan, whose values, planes and tie-breaks are bitwise the cache's, and without the
+    // speculative searches that read only the cache (run_solver, ipm_loop, run_resto).
+    bool fits = false;
+    for (int attempt = 0; attempt < 3; attempt++) {
         hipLaunchKernelGGL(plane_cache_kernel, dim3(p->T, p->W), dim3(EVAL_THREADS), 0, p->stream, d);
         if (hipMemcpyAsync(p->h_pcnext, d.pcnext, sizeof(unsigned), hipMemcpyDeviceToHost, p->stream) != hipSuccess ||
             hipStreamSynchronize(p->stream) != hipSuccess)
             break;
         const long need = (long)*p->h_pcnext;
-        if (need <= d.pc_pool) break;
+        (void)hipMemsetAsync(d.pcnext, 0, sizeof(unsigned), p->stream);
+        if (need <= d.pc_pool) {
+            fits = true;
+            break;
+        }
+        if (attempt == 2) break;
         const long grow = need + need / 4;
         double* pc = nullptr;
         uint16_t* pcp = nullptr;
-        if (dalloc(&pc, 5 * (size_t)grow) != hipSuccess) break;
+        if (std::getenv("ARMOUR_PC_GROW_FAIL") || dalloc(&pc, 5 * (size_t)grow) != hipSuccess) break;
         if (dalloc(&pcp, (size_t)grow) != hipSuccess) { (void)hipFree(pc); break; }
         for (void*& a : p->allocs) {
             if (a == (void*)d.pc) { (void)hipFree(a); a = pc; }
@@ -798,9 +812,8 @@ static void ensure_plane_cache(armour_planner* p) {
         d.pc = pc;
         d.pcp = pcp;
         d.pc_pool = grow;
-        (void)hipMemsetAsync(d.pcnext, 0, sizeof(unsigned), p->stream);
     }
-    d.pcready = 1;
+    d.pcready = fits ? 1 : 0;
 }
 
 static int nside_count(const armour_planner* p) {
@@ -850,7 +863,7 @@ static int ipm_loop(armour_planner* p, int nrun) {
     // still in a phase when the loop ends finish it after the loop (run_solver: run_resto), and so
     // does a restarted world's interior point (the next ipm_loop). A loop over one world runs its
     // phases after the loop: there is no other world's iteration to overlap them with.
-    const bool inl = p->resto_inline && nrun > 1;
+    const bool inl = p->resto_inline && d.pcready && nrun > 1;
     int* RL = p->d_lists + 4 * p->Wmax;
     int* PL = p->d_lists + 5 * p->Wmax;
     volatile int* flr = p->h_flags;
@@ -1073,7 +1086,7 @@ static int run_resto(armour_planner* p, const int* list, int n) {
     dr.b_in_cs = 0;
     const volatile int* fl = p->h_flags;
     const int guard = 4 * (dr.opt.max_iter + 1);
-    if (p->resto_spec) {
+    if (p->resto_spec && p->d.pcready) {
         // iteration k works on list L[k & 1] (the first: `list`, n entries); resto_world_Vs appends
         // the worlds still in the phase to L[(k + 1) & 1] and stores its length in cnt[8 + ((k + 1) & 1)]
         // (the next launches' lcount) and flags[2 + (k & 1)] (read by the host after iteration k + 1

@@ -75,17 +75,20 @@ def test_bench_step_matches_oracle_world_by_world():
     print(f"bench step: {W} worlds, {n_feas} feasible; identical iteration counts {W - len(it_diff)}/{W}; "
           f"converged/feasible k_opt within 1e-8: {int(okm.sum()) - len(k_diff)}/{int(okm.sum())} "
           f"(max {dk[okm].max():.1e}); infeasible plans' k_opt (not an output) max |dk| {dk[~okm].max():.1e}")
-    # Bar: every decision identical (above); at least 99 % of the worlds on the oracle's exact
+    # Bar: every decision identical (above); at least 99.5 % of the worlds on the oracle's exact
     # solver path (same iteration count, k_opt within 1e-8). The rest are long solves through
     # ill-conditioned Newton systems, where ~1e-14 differences of g / J (summation order of the
     # reach engines) grow to a different path: a converged or feasible plan within 10 iterations
     # and within the solver's tolerance scale (k_opt 1e-4, cost 1e-6 relative). An infeasible
-    # plan's output is -1 whatever iteration its line search gives up at, so its iteration count
-    # is reported, not bounded. Observed (r05, 3924 worlds): 7 off the path, 5 infeasible
-    # line-search failures (1, 1, 1, 2 and 34 iterations apart) and two 31-iteration converged
-    # plans 3.6e-8 and 1.4e-7 away.
-    assert len(set(it_diff) | set(k_diff)) <= W // 100
+    # plan's output is -1 whatever iteration its line search gives up at; its iteration count is
+    # held to within 40 of the oracle's (the largest gap observed is 34). Observed (r05, 3924
+    # worlds): 7 off the path, 5 infeasible line-search failures (1, 1, 1, 2 and 34 iterations
+    # apart) and two 31-iteration converged plans 3.6e-8 and 1.4e-7 away. The seeds off the path
+    # are printed above (the set moves with rounding-level changes of the evaluation's arithmetic,
+    # so it is bounded, not frozen).
+    assert len(set(it_diff) | set(k_diff)) <= W // 200
     assert all(abs(res[i]["iterations"] - int(fx["iterations"][i])) <= 10 for i in it_diff if ok[i])
+    assert all(abs(res[i]["iterations"] - int(fx["iterations"][i])) <= 40 for i in it_diff)
     assert dk[okm].max() <= 1e-4 and dcost[okm].max() <= 1e-6
     # the converged plans' KKT error (Ipopt-scaled, as the solver's stopping test) is within tol
     kkt = np.array([r["kkt"] for r in res])

@@ -112,3 +112,29 @@ def test_plane_cache_pool_regrows():
     assert st["blocks_cached"] == st["blocks"] and st["pool_records"] >= st["planes_kept"] > W * T * 7 * O
     check_plan(S, Q, worlds)
     check_plan(P, S, worlds)
+
+
+def test_plane_cache_grow_failure_falls_back_to_full_scan():
+    """A build that overflows its pool when the larger pool cannot be allocated
+    (ARMOUR_PC_GROW_FAIL simulates the failed allocation) must not leave the cache marked ready:
+    the blocks that did not fit have no records at their pool offset. The solve then runs on the
+    full scan and the sequential line-search rounds: every plan, constraint value and iteration
+    count bitwise those of the full-scan planner, and a later build that fits caches again."""
+    T, O, W = 100, 20, 8
+    worlds = [A.make_world(3100 + s, O, profile="survey") for s in range(W)]
+    P, Q = planners(T, O, W)
+    with env("ARMOUR_PC_K", "1"):
+        S = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    with env("ARMOUR_PC_GROW_FAIL", "1"):
+        check_plan(S, Q, worlds)
+        S.reach(worlds)
+        st = S.plane_cache_stats()
+        assert st["blocks_cached"] < st["blocks"]
+        rng = np.random.default_rng(5)
+        for x in points(rng, 2):
+            for w in range(W):
+                g, J = S.eval_constraints(w, x)
+                gq, Jq = Q.eval_constraints(w, x)
+                np.testing.assert_array_equal(g, gq)
+                np.testing.assert_array_equal(J, Jq)
+    check_plan(S, P, worlds)
