@@ -276,6 +276,7 @@ int oracle_plan_ex(void* h, double* k_opt, double* g_out, double* stats, int max
     opt.mu_strategy = mu_strategy;
     opt.mu_study = flags & 3;
     opt.qf_grid = (flags >> 8) & 255;  // studies: bits 8-15
+    opt.lbfgs_hist = (flags >> 16) & 255;  // studies: bits 16-23 (0: the product's damped BFGS)
     if (flags & 4) opt.resto_max = 0;  // no restoration phase (studies)
     double x[NF] = {0, 0, 0, 0, 0, 0, 0};  // NLPclass.cu:193-199
     std::vector<double> g(P->m());

@@ -121,6 +121,28 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
     double H[NMAX * NMAX] = {0};
     for (int j = 0; j < n; j++) H[j * n + j] = 1.0;
     bool first_update = true;
+    // limited-memory BFGS (opt.lbfgs_hist > 0, study only): the stored (s, y) pairs, oldest first;
+    // H is rebuilt after every update as sigma I followed by the BFGS updates of the stored pairs in
+    // order, the dense form of the compact representation
+    std::vector<std::vector<double>> lb_s, lb_y;
+    int lb_skips = 0;
+    auto lbfgs_rebuild = [&](double sigma) {
+        for (int i = 0; i < n * n; i++) H[i] = 0;
+        for (int j = 0; j < n; j++) H[j * n + j] = sigma;
+        for (size_t q = 0; q < lb_s.size(); q++) {
+            const double* sv = lb_s[q].data();
+            const double* y = lb_y[q].data();
+            double Hs[NMAX], sHs = 0, sy = 0;
+            for (int i = 0; i < n; i++) {
+                Hs[i] = 0;
+                for (int j = 0; j < n; j++) Hs[i] += H[i * n + j] * sv[j];
+                sHs += sv[i] * Hs[i];
+                sy += sv[i] * y[i];
+            }
+            for (int i = 0; i < n; i++)
+                for (int j = 0; j < n; j++) H[i * n + j] += -Hs[i] * Hs[j] / sHs + y[i] * y[j] / sy;
+        }
+    };
     std::vector<double> filt_theta, filt_phi;
     double theta_max = -1, theta_min = -1;
     int nfail = 0;
@@ -597,6 +619,9 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             init_slacks();
             for (int i = 0; i < n * n; i++) H[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
             first_update = true;
+            lb_s.clear();
+            lb_y.clear();
+            lb_skips = 0;
             filt_theta.clear();
             filt_phi.clear();
             theta_max = -1;
@@ -632,8 +657,36 @@ IpmResult ipm_solve(IpmProblem& prob, const IpmOptions& opt, double* x, double* 
             grow(Jt, r, at);
             for (int j = 0; j < n; j++) wa_new[j] += w * at[j];
         }
+        if (opt.lbfgs_hist > 0) {
+            // Ipopt's limited-memory BFGS of the Lagrangian Hessian (study only)
+            std::vector<double> sv(n), y(n);
+            double ss = 0, yy = 0, sy = 0;
+            for (int j = 0; j < n; j++) {
+                sv[j] = xt[j] - x[j];
+                y[j] = (gradt[j] - grad[j]) - (wa_new[j] - wa_old[j]);
+                ss += sv[j] * sv[j];
+                yy += y[j] * y[j];
+                sy += sv[j] * y[j];
+            }
+            if (sy <= std::sqrt(2.220446049250313e-16) * std::sqrt(ss) * std::sqrt(yy) || ss <= 0) {
+                if (++lb_skips > 2) {
+                    lb_s.clear();
+                    lb_y.clear();
+                    lb_skips = 0;
+                    lbfgs_rebuild(1.0);
+                }
+            } else {
+                lb_skips = 0;
+                if ((int)lb_s.size() == opt.lbfgs_hist) {
+                    lb_s.erase(lb_s.begin());
+                    lb_y.erase(lb_y.begin());
+                }
+                lb_s.push_back(sv);
+                lb_y.push_back(y);
+                lbfgs_rebuild(std::min(std::max(sy / ss, 1e-8), 1e8));
+            }
+        } else {
         // damped BFGS on the Lagrangian Hessian
-        {
             double sv[NMAX], y[NMAX], Hs[NMAX];
             double ss = 0;
             for (int j = 0; j < n; j++) {

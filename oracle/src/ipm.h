@@ -49,6 +49,13 @@ struct IpmOptions {
     // studies of the adaptive rule only (tools/mu_sensitivity.py): bit 0 drops the 2^(1/8) grid
     // (ipm.cpp mu_grid), bit 1 the tol / 10 floor (Ipopt's mu_min 1e-11 instead)
     int mu_study = 0;
+    // Hessian approximation (pricing study only, not on the device): 0 the product's damped BFGS
+    // matrix; h > 0 Ipopt's limited-memory BFGS (hessian_approximation limited-memory,
+    // KPR/armour_main.cu:259), restated from its documented options: history h (Ipopt's
+    // limited_memory_max_history default 6), update type bfgs, initialisation scalar1
+    // (sigma = s'y / s's, clamped to [1e-8, 1e8]), a pair skipped when s'y <= sqrt(eps) |s| |y|
+    // and the history reset after more than limited_memory_max_skipping = 2 skips in a row
+    int lbfgs_hist = 0;
     // restoration phase (ipm.cpp restoration): phases per solve (0: none; a failed line search
     // then takes the last trial, and three in a row end the solve), violation target inside the
     // bounds, box barrier weight, stall ratio

@@ -21,6 +21,13 @@ for p in ("armour-dev_amd", "oracle", "tests"):
 # (mu_strategy, IpmOptions::mu_study): the product's adaptive rule is (1, 0); bit 0 drops its
 # 2^(1/8) grid, bit 1 its tol / 10 floor (Ipopt's mu_min 1e-11)
 VARIANTS = {"monotone": (0, 0), "adaptive_ipopt_floor": (1, 3), "adaptive_floor": (1, 1), "adaptive": (1, 0)}
+# round 6: the candidate device rules — the product's rule with L-BFGS(6)
+# (flags bits 16-23), Ipopt's quality-function pair with the product's floor and grid on a 16-point
+# sigma grid (mu_strategy 3, flags bits 8-15), the same with L-BFGS(6), and Ipopt's pair as Ipopt
+# sets it with L-BFGS(6) (the reference's configuration); MU_VARIANTS=r06 selects them
+if os.environ.get("MU_VARIANTS") == "r06":
+    VARIANTS = {"adaptive": (1, 0), "adaptive_lbfgs6": (1, 6 << 16), "qf_s3_g16": (3, 16 << 8),
+                "qf_s3_g16_lbfgs6": (3, (16 << 8) | (6 << 16)), "reference_config": (2, 6 << 16)}
 NOISE = 1e-15
 
 
