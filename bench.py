@@ -511,9 +511,14 @@ def main():
                           max_iter=3000)
             long_res, _ = L.plan([flat[i] for i in capped])
             L.close()
+            f100 = [int(i) for i in capped if res[i]["feasible"]]
+            f3000 = [int(i) for r, i in zip(long_res, capped) if r["feasible"]]
             line["solver"]["iteration_limit_study"] = {
-                "worlds": len(capped), "feasible_at_100": int(sum(res[i]["feasible"] for i in capped)),
-                "feasible_at_3000": int(sum(r["feasible"] for r in long_res)),
+                "worlds": len(capped), "feasible_at_100": len(f100), "feasible_at_3000": len(f3000),
+                # which capped worlds are feasible (step indices), not only how many: the verdicts
+                # agree world by world when the two lists are equal
+                "feasible_worlds_at_100": f100, "feasible_worlds_at_3000": f3000,
+                "same_worlds_feasible": f100 == f3000,
                 "iterations_at_3000": [int(r["iterations"]) for r in long_res],
                 "status_at_3000": [int(r["status"]) for r in long_res],
                 "cost_delta": [float(r["cost"] - res[i]["cost"]) for r, i in zip(long_res, capped)]}
