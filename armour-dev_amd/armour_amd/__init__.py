@@ -108,6 +108,7 @@ def lib():
                                                  ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         L.armour_get_joint_bounds.argtypes = [ctypes.c_void_p, _dp]
         L.armour_get_plane_cache_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
+        L.armour_get_reach_span.argtypes = [ctypes.c_void_p, _dp]
         L.armour_get_reach_dump.argtypes = [ctypes.c_void_p, _dp, ctypes.c_int]
         L.armour_get_reach_profile.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
         for name in ("armour_get_constraints", "armour_get_link_centers", "armour_get_link_generators",
@@ -124,7 +125,7 @@ ABI_SYMBOLS = ["armour_copy_bandwidth", "armour_create", "armour_create_robot", 
                "armour_num_joints", "armour_get_joint_bounds", "armour_get_reach_program", "armour_get_reach_profile",
                "armour_get_reach_dump", "armour_get_reach_occupancy", "armour_get_monomial_counts",
                "armour_create_armtd", "armour_plan_armtd_batch", "armour_reach_armtd_batch",
-               "armour_get_plane_cache_stats", "armour_plan"]
+               "armour_get_plane_cache_stats", "armour_plan", "armour_get_reach_span"]
 
 
 def default_batch(T: int, device: int = 0, waves: int = 2) -> int:
@@ -225,7 +226,7 @@ class Planner:
         res = (Result * len(worlds))()
         tm = Timing()
         _check(self._plan_call(self.h, len(worlds), arr, res, ctypes.byref(tm)))
-        return self._results(res), tm.as_dict()
+        return self._results(res), self._span(tm.as_dict())
 
     def _plan_call(self, *a):
         return lib().armour_plan_batch(*a)
@@ -243,7 +244,14 @@ class Planner:
         arr = self._worlds(worlds)
         tm = Timing()
         _check(self._reach_call(self.h, len(worlds), arr, ctypes.byref(tm)))
-        return tm.as_dict()
+        return self._span(tm.as_dict())
+
+    def _span(self, tm):
+        # the reach launch's device-clock execution span (armour_get_reach_span; -1 when unknown)
+        v = ctypes.c_double(-1.0)
+        rc = lib().armour_get_reach_span(self.h, ctypes.byref(v))
+        tm["reach_span_ms"] = v.value if rc == 0 else -1.0
+        return tm
 
     def _reach_call(self, *a):
         return lib().armour_reach_batch(*a)
@@ -325,6 +333,12 @@ class Planner:
         rc = lib().armour_get_reach_occupancy(self.h, used, caps, n)
         _check(min(0, rc))
         return {k: (int(used[i]), int(caps[i])) for i, k in enumerate(self.OCCUPANCY)}
+
+    def reach_span_ms(self):
+        """device-clock execution span of the last reach launch, ms (armour_get_reach_span)"""
+        v = ctypes.c_double()
+        _check(lib().armour_get_reach_span(self.h, ctypes.byref(v)))
+        return v.value
 
     def plane_cache_stats(self):
         """certified plane cache of the current reach sets (armour_get_plane_cache_stats)"""

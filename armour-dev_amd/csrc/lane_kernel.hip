@@ -72,6 +72,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(LT, LT), amdgpu_waves_per_
     __shared__ int occ[4];
     __shared__ int last;
 
+    span_start(a.rc);
     const RobotParams& rp = *rpp;
     const long wg = blockIdx.x;
     LCtx x;

@@ -62,17 +62,14 @@ struct armour_planner {
     // reach program (ProgramBuilder::ops) on the device
     Op* d_prog = nullptr;
     int* d_slot_off = nullptr;
-    uint64_t* d_live = nullptr;   // [nops][2] ProgramBuilder::live_masks (the LDS-arena reach kernel)
-    bool lds_arena = false;       // batches of at most one job per CU on the LDS-arena kernel (ARMOUR_LDS_ARENA=1; measured
-                                  // no faster than the HBM arena)
-    int last_lds_fallback = 0;    // the last reach ran again on the HBM arena (a job outgrew the LDS arena)
-    bool lds_trace = false;       // ARMOUR_LDS_TRACE=1: report LDS-arena overflows on stderr (diagnostics)
     JrsJoint* d_jrs = nullptr;
     int nops = 0, nslots = 0;
     unsigned long long* d_bytes = nullptr;
     unsigned long long* d_prof = nullptr;  // per-op [cycles, terms] when ARMOUR_PROFILE_OPS is set
     double* d_dump = nullptr;              // op-by-op state of job 0 when ARMOUR_DUMP_OPS is set
     double last_kernel_ms = 0, last_bytes = 0;
+    double last_span_ms = -1;  // device-clock execution span of the last reach launch (armour_get_reach_span)
+    int wall_khz = 0;          // hipDeviceAttributeWallClockRate
     unsigned long long* d_occ = nullptr;   // [8] reach capacity use of the last launch (ReachCounters)
     unsigned* d_done = nullptr;            // workgroups finished in the current reach launch
     long long* h_sum = nullptr;            // mapped host: reach counters published by the last workgroup
@@ -172,6 +169,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     // ARMOUR_DEVICE_SHARED=1 (it only chooses the bundle kernel's shape)
     if (const char* e = std::getenv("ARMOUR_DEVICE_SHARED")) p->device_shared = std::atoi(e) != 0;
     HIPCK(hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    if (hipDeviceGetAttribute(&p->wall_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) p->wall_khz = 0;
     if (robot) {
         if (!robot_from_tables(*robot, p->rp))
             return fail(ARMOUR_E_ARG, "invalid robot tables (num_joints 7..9, actuated joints first, M_min > 0, K > 0)");
@@ -261,10 +259,6 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
             return rc;
         HIPCK(hipMemcpy(p->d_prog, pb.ops.data(), sizeof(Op) * pb.ops.size(), hipMemcpyHostToDevice));
         HIPCK(hipMemcpy(p->d_slot_off, off.data(), sizeof(int) * off.size(), hipMemcpyHostToDevice));
-        // live slots at each op, for the per-job engine's LDS arena (reach_kernel<256, true>)
-        const std::vector<uint64_t> live = pb.live_masks();
-        if ((rc = p->alloc(&p->d_live, live.size()))) return rc;
-        HIPCK(hipMemcpy(p->d_live, live.data(), sizeof(uint64_t) * live.size(), hipMemcpyHostToDevice));
         if (std::getenv("ARMOUR_PROFILE_OPS")) {
             // =3: no op profiling; [start, end] wall clock (100 MHz) of every bundle of the last launch
             // after the op tables (bundle-engine load balance)
@@ -312,16 +306,6 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     ra.slot_off = p->d_slot_off;
     ra.nslots = p->nslots;
     ra.bytes = p->d_bytes;
-    ra.live = p->d_live;
-    if (const char* e = std::getenv("ARMOUR_LDS_ARENA")) p->lds_arena = std::atoi(e) != 0;
-    if (const char* e = std::getenv("ARMOUR_LDS_TRACE")) p->lds_trace = std::atoi(e) != 0;
-    // ARMOUR_LDS_ARENA_SCALE=k (tests): 1/k of the LDS arena, to exercise the HBM fallback
-    {
-        const char* e = std::getenv("ARMOUR_LDS_ARENA_SCALE");
-        const int k = e ? std::max(1, std::atoi(e)) : 1;
-        ra.lds_h = LDS_ARENA_H / k;
-        ra.lds_c = LDS_ARENA_C / k;
-    }
     // ARMOUR_PROFILE_OPS=1: per-op cycles/terms; =2: phase totals (each distorts the other)
     const char* pm = std::getenv("ARMOUR_PROFILE_OPS");
     ra.prof = (pm && std::atoi(pm) == 2) ? nullptr : p->d_prof;
@@ -646,8 +630,6 @@ static int run_reach(armour_planner* p) {
     const long jobs = (long)p->W * p->T;
     const int grid = (int)(jobs < p->reach_grid ? jobs : p->reach_grid);
     p->lane_engine = !(p->has_job && jobs <= p->job_max);
-    const bool lds = !p->lane_engine && p->lds_arena && !p->job_narrow && jobs <= p->ncu && !ra.dump;
-    p->last_lds_fallback = 0;
     const long nj = jobs * NF;
     HIPCK(hipEventRecord(p->ev[3], rs));
     if (p->armtd)
@@ -670,11 +652,8 @@ static int run_reach(armour_planner* p) {
         const int lg = (int)(bundles < slots ? bundles : slots);
         launch_lane(shape, lg, rs, p->d_rp, la, p->ro);
     } else {
-        // a batch of at most one job per CU takes the LDS-arena kernel, one that fits the chip in one
-        // round at two jobs per CU the wide kernel
-        if (lds)
-            hipLaunchKernelGGL((reach_kernel<REACH_WIDE_THREADS, true>), dim3((int)jobs), dim3(REACH_WIDE_THREADS), 0, rs, p->d_rp, ra, p->ro);
-        else if (jobs <= (long)REACH_WIDE_PER_CU * p->ncu && !p->job_narrow)
+        // a batch that fits the chip in one round at two jobs per CU takes the wide kernel
+        if (jobs <= (long)REACH_WIDE_PER_CU * p->ncu && !p->job_narrow)
             hipLaunchKernelGGL(reach_kernel<REACH_WIDE_THREADS>, dim3(grid), dim3(REACH_WIDE_THREADS), 0, rs, p->d_rp, ra, p->ro);
         else
             hipLaunchKernelGGL(reach_kernel<REACH_THREADS>, dim3(grid), dim3(REACH_THREADS), 0, rs, p->d_rp, ra, p->ro);
@@ -687,29 +666,13 @@ static int run_reach(armour_planner* p) {
         return fail(ARMOUR_E_HIP, "reach kernel finished without publishing its counters (sequence number mismatch)");
     std::vector<int> err(p->W);
     for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
-    if (lds && std::any_of(err.begin(), err.end(), [](int e) { return (e & ERR_ARENA) != 0; })) {
-        // a job's live values outgrew the LDS arena: the batch again on the HBM arena (jrs_kernel
-        // zeroes the counters; the JRS scalars come out the same)
-        p->last_lds_fallback = 1;
-        if (p->lds_trace) {
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, p->ev[3], p->ev[4]);
-            int nw = 0;
-            for (int w = 0; w < p->W; w++) nw += (err[w] & ERR_ARENA) != 0;
-            std::fprintf(stderr, "armour: LDS arena overflow in %d of %d worlds (launch %.3f ms), HBM rerun\n", nw, p->W, ms);
-        }
-        ra.rc.seq = ++p->reach_seq;
-        hipLaunchKernelGGL(jrs_kernel, dim3((int)((jobs * NF + 127) / 128)), dim3(128), 0, rs, p->d_rp, p->W, p->T, p->q0, p->qd0,
-                           p->qdd0, p->d_jrs, p->rc, p->ro.err);
-        hipLaunchKernelGGL(reach_kernel<REACH_WIDE_THREADS>, dim3(grid), dim3(REACH_WIDE_THREADS), 0, rs, p->d_rp, ra, p->ro);
-        HIPCK(hipGetLastError());
-        HIPCK(hipEventRecord(p->ev[4], rs));
-        HIPCK(hipEventSynchronize(p->ev[4]));
-        if (sum[RSUM_SEQ] != p->reach_seq)
-            return fail(ARMOUR_E_HIP, "reach kernel finished without publishing its counters (sequence number mismatch)");
-        for (int w = 0; w < p->W; w++) err[w] = (int)sum[RSUM_ERR + w];
-    }
     for (int k = 0; k < 8; k++) p->h_occ[k] = (unsigned long long)sum[1 + k];
+    {
+        // the launch's execution span on the device clock (reach_kernel.hip span_start): occ[5]
+        // holds ~(first workgroup start), occ[6] the last workgroup's end
+        const unsigned long long t0 = ~p->h_occ[5], t1 = p->h_occ[6];
+        p->last_span_ms = (p->h_occ[5] != 0 && t1 >= t0 && p->wall_khz > 0) ? (double)(t1 - t0) / p->wall_khz : -1.0;
+    }
     {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, p->ev[3], p->ev[4]);
@@ -1589,6 +1552,13 @@ int armour_get_monomial_counts(armour_planner* p, int w, int* link_counts, int* 
     if (torque_counts)
         HIPCK(hipMemcpy(torque_counts, p->ro.tq_cnt + j0 * NF, sizeof(int) * p->T * NF, hipMemcpyDeviceToHost));
     return 0;
+}
+
+int armour_get_reach_span(armour_planner* p, double* span_ms) {
+    if (!p || !span_ms) return fail(ARMOUR_E_ARG, "null planner or output");
+    if (!p->reached) return fail(ARMOUR_E_STATE, "no reach set");
+    *span_ms = p->last_span_ms;
+    return p->last_span_ms >= 0 ? 0 : fail(ARMOUR_E_STATE, "no device clock span for the last reach");
 }
 
 int armour_get_plane_cache_stats(armour_planner* p, long long* out, int n) {

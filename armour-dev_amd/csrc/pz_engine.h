@@ -33,9 +33,6 @@
 
 namespace armour {
 constexpr int MAX_SLOTS = 96;  // handle slots of a reach program (ProgramBuilder)
-#ifndef PZ_PREFIX_CHECK
-#define PZ_PREFIX_CHECK 0      // 1: arena_compact also forms the block offsets serially and reports mismatches
-#endif
 }
 
 #define AI __host__ __device__ inline __attribute__((always_inline))
@@ -72,11 +69,6 @@ struct Arena {
     long hcap, ccap;
     long hused, cused;
     double bytes;  // algorithmic monomial bytes read + written by the operators of this job
-    // LDS-resident arena (reach_kernel's single-round variant): compacted to the live values when
-    // an op may not fit (arena_ensure, Ctx::live). lds = 0: bump allocation only (HBM arena)
-    int lds;
-    int ncompact;   // compactions and coefficient rows moved (diagnostics)
-    long cmoved;
 };
 
 struct Ctx {
@@ -84,12 +76,9 @@ struct Ctx {
     PZH* H;            // handle table (LDS)
     double* pool;      // handle payload pool (LDS)
     Arena* A;          // bump arena state (LDS)
-    // arena storage: HBM, or the LDS arrays of reach_kernel<NT, true>. Held here (registers), set
-    // from the kernel's own arrays, so the compiler sees their address space: LDS accesses compile
-    // to ds_read / ds_write, not flat instructions (which take the vector-memory path)
+    // arena storage (HBM, per workgroup), held here (registers)
     uint64_t* ah;
     double* ac;
-    const uint64_t* live;  // LDS arena: per op, the slots live at its start (ProgramBuilder::live_masks)
     uint64_t* kh;      // ordered keys: hash        (LDS, cap_lds entries)
     uint32_t* ki;      // ordered keys: term index
     int* kp;           // keep flags / scan
@@ -107,8 +96,6 @@ struct Ctx {
     double thr;
     unsigned long long* phase;  // optional large-operator phase cycle counters [8] (profiling)
     int mode;          // diagnostics: bit 0 = no wave-0 path
-    int pc;            // LDS arena: the op being run (its live mask, for a compaction inside it)
-    long bud_h, bud_c; // LDS arena: room every thread knows to be free (run_program)
 };
 
 enum : int { ERR_ARENA = 1, ERR_SORTCAP = 2, ERR_LINKGEN = 4, ERR_OUTCAP = 8, ERR_HANDLES = 16 };
@@ -473,11 +460,10 @@ struct Terms {
 };
 
 // copy the sources into LDS (hashes, then effective coefficient rows), if they fit; else the
-// hashes alone, if they fit (HBM arena only) (the key order's searches are chains of dependent hash loads, the
+// hashes alone, if they fit (the key order's searches are chains of dependent hash loads, the
 // group passes' coefficient loads are independent). Uniform decision; the caller's barrier
 // publishes the staged copy.
 AI void stage_sources(Ctx& x, Terms& T) {
-    if (x.A->lds) return;  // the LDS arena: the sources are in LDS already (views read in place)
     int need = 0, need_h = 0;
     UNR for (int s = 0; s < 3; s++) if (s < T.ns) { need += T.S[s].cnt * (1 + T.S[s].n); need_h += T.S[s].cnt; }
     if (need_h > x.stage_cap) return;
@@ -573,201 +559,6 @@ AI void arena_alloc_t0(Ctx& x, PZH& h, int K, int stride) {
         h.coff = c0;
         h.cnt = K;
     }
-}
-
-// LDS arena: move the blocks of the values live at op pc (their handles' hashes and coefficient
-// rows; views share their parent's block) to the bottom of the arena in allocation order and
-// repoint the handles; every thread of the group, at an op boundary (no operand pointer is held).
-// Owners and ranks in parallel over the MAX_SLOTS handles: a block's owner is its lowest live slot, its
-// rank the number of distinct live blocks below it, its new offsets the sizes of the blocks ranked
-// before it. The hash and coefficient parts are ranked separately, each by its own offset: ops of
-// different waves allocate concurrently (arena_alloc_t0 from each wave's lane 0: two atomics), so
-// two blocks' hash parts can lie in the other order than their coefficient parts, and a move in one
-// part's order would overwrite the other part's sources. Blocks below the first one that moves stay
-// where they are. Moves in chunks of four elements per thread: all reads of a chunk before a
-// barrier, then the writes; a block only moves down, so a chunk's writes never reach the next
-// chunk's sources.
-__device__ __host__ __attribute__((noinline)) void arena_compact(Ctx& x, int pc, long* used_h = nullptr, long* used_c = nullptr) {
-    Arena& A = *x.A;
-    const Grp& g = x.g;
-    long* tb = reinterpret_cast<long*>(x.stage);  // slot and block tables (the stage is free here)
-    long *key = tb, *shc = tb + MAX_SLOTS, *scc = tb + 2 * MAX_SLOTS;  // per slot: block hoff (-1: none), sizes
-    long *boh = tb + 3 * MAX_SLOTS, *bhc = tb + 4 * MAX_SLOTS, *boc = tb + 5 * MAX_SLOTS;  // per rank
-    long *bcc = tb + 6 * MAX_SLOTS, *bnh = tb + 7 * MAX_SLOTS, *bnc = tb + 8 * MAX_SLOTS;
-    long* ckey = tb + 9 * MAX_SLOTS;  // per slot: block coff (-1: none)
-#ifdef REACH_CFG_STAGE
-    static_assert(10 * MAX_SLOTS * sizeof(long) + (3 * MAX_SLOTS + 3) * sizeof(int) <= REACH_CFG_STAGE * sizeof(double),
-                  "compaction tables");
-#endif
-    // the int tables after the long ones, also in the stage: a compaction inside a simplify (after
-    // its key scan) must leave the op's keys and positions (x.kh / x.ki / x.kp) alone
-    int* own = reinterpret_cast<int*>(tb + 10 * MAX_SLOTS);  // [MAX_SLOTS] owner flags
-    int* rank = own + MAX_SLOTS;      // [MAX_SLOTS] hash-part rank
-    int* crank = own + 2 * MAX_SLOTS; // [MAX_SLOTS] coefficient-part rank
-    int* misc = own + 3 * MAX_SLOTS;  // block count, first hash / coefficient block that moves
-    constexpr int B = 16;             // table reads per batch (independent loads in flight)
-    static_assert(MAX_SLOTS % B == 0, "slot batches");
-    const uint64_t l0 = x.live[2 * pc], l1 = x.live[2 * pc + 1];
-    g.sync();
-    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        const bool lv = ((q < 64 ? l0 >> q : l1 >> (q - 64)) & 1ull) && x.H[q].cnt > 0;
-        key[q] = lv ? x.H[q].hoff : -1;
-        ckey[q] = lv ? x.H[q].coff : -1;
-        shc[q] = x.H[q].cnt;
-        scc[q] = (long)x.H[q].cnt * x.H[q].stride;
-    }
-    if (g.tid == 0) { misc[0] = 0; misc[1] = MAX_SLOTS; misc[2] = MAX_SLOTS; }
-    g.sync();
-    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        const long kq = key[q];
-        bool o = kq >= 0;
-        for (int r0 = 0; r0 < MAX_SLOTS; r0 += B) {
-            long kr[B];
-            UNR for (int u = 0; u < B; u++) kr[u] = key[r0 + u];
-            UNR for (int u = 0; u < B; u++) o = o && !(r0 + u < q && kr[u] == kq);
-        }
-        own[q] = o ? 1 : 0;
-    }
-    g.sync();
-    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        const long kq = key[q], cq = ckey[q];
-        if (kq < 0) continue;
-        int rk = 0, rc = 0;
-        for (int r0 = 0; r0 < MAX_SLOTS; r0 += B) {
-            long kr[B], cr[B];
-            int orr[B];
-            UNR for (int u = 0; u < B; u++) { kr[u] = key[r0 + u]; cr[u] = ckey[r0 + u]; orr[u] = own[r0 + u]; }
-            UNR for (int u = 0; u < B; u++) {
-                rk += (orr[u] && kr[u] < kq) ? 1 : 0;
-                rc += (orr[u] && cr[u] >= 0 && cr[u] < cq) ? 1 : 0;
-            }
-        }
-        rank[q] = rk;
-        crank[q] = rc;
-        if (own[q]) {
-            boh[rk] = kq;
-            bhc[rk] = shc[q];
-            boc[rc] = cq;
-            bcc[rc] = scc[q];
-            int_add(&misc[0], 1);
-        }
-    }
-    g.sync();
-    const int nb = misc[0];
-    // New block offsets: a parallel prefix per part, each thread summing the sizes of the ranks below
-    // its own (16 independent table reads in flight); PZ_PREFIX_CHECK=1 also forms them serially and
-    // reports any difference.
-    for (int i = g.tid; i < nb; i += g.n) {
-        long sh = 0, sc = 0;
-        for (int r0 = 0; r0 < i; r0 += B) {
-            long hr[B], cr[B];
-            UNR for (int u = 0; u < B; u++) { const int r = min(r0 + u, MAX_SLOTS - 1); hr[u] = bhc[r]; cr[u] = bcc[r]; }
-            UNR for (int u = 0; u < B; u++) if (r0 + u < i) { sh += hr[u]; sc += cr[u]; }
-        }
-        bnh[i] = sh;
-        bnc[i] = sc;
-        if (sh != boh[i]) int_min(&misc[1], i);
-        if (sc != boc[i]) int_min(&misc[2], i);
-        if (i == nb - 1) {
-            A.hused = sh + bhc[i];
-            A.cused = sc + bcc[i];
-        }
-    }
-    if (g.tid == 0) {
-        if (nb == 0) {
-            A.hused = 0;
-            A.cused = 0;
-        }
-        A.ncompact++;
-    }
-    g.sync();
-#if PZ_PREFIX_CHECK
-    if (g.tid == 0) {
-        long th0 = 0, tc0 = 0;
-        int fh = MAX_SLOTS, fc = MAX_SLOTS;
-        for (int r = 0; r < nb; r++) {
-            if (bnh[r] != th0 || bnc[r] != tc0)
-                printf("prefix mismatch: block %d pc %d rank %d of %d: parallel (%ld, %ld) serial (%ld, %ld)\n",
-                       (int)blockIdx.x, pc, r, nb, bnh[r], bnc[r], th0, tc0);
-            if (th0 != boh[r] && r < fh) fh = r;
-            if (tc0 != boc[r] && r < fc) fc = r;
-            th0 += bhc[r];
-            tc0 += bcc[r];
-        }
-        if (fh != misc[1] || fc != misc[2] || th0 != A.hused || tc0 != A.cused)
-            printf("prefix mismatch: block %d pc %d first %d %d / %d %d, used (%ld, %ld) / (%ld, %ld)\n", (int)blockIdx.x,
-                   pc, misc[1], misc[2], fh, fc, A.hused, A.cused, th0, tc0);
-    }
-    g.sync();
-#endif
-    const int first_h = misc[1], first_c = misc[2];
-    const long th = A.hused, tc = A.cused;
-    if (used_h) { *used_h = th; *used_c = tc; }  // read by every thread before the final barrier
-    if (g.tid == 0 && first_c < nb) A.cmoved += tc - bnc[first_c];
-    auto block_of = [&](const long* pre, int first, long q) {  // the last block whose compacted start <= q
-        int lo = first, hi = nb - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (pre[mid] <= q) lo = mid; else hi = mid - 1;
-        }
-        return lo;
-    };
-    constexpr int E = 4;
-    if (first_h < nb) {
-        for (long base = bnh[first_h]; base < th; base += (long)E * g.n) {
-            uint64_t v[E];
-            UNR for (int e = 0; e < E; e++) {
-                const long q = base + g.tid + (long)e * g.n;
-                v[e] = 0;
-                if (q < th) { const int r = block_of(bnh, first_h, q); v[e] = x.ah[boh[r] + (q - bnh[r])]; }
-            }
-            g.sync();
-            UNR for (int e = 0; e < E; e++) {
-                const long q = base + g.tid + (long)e * g.n;
-                if (q < th) x.ah[q] = v[e];
-            }
-            g.sync();
-        }
-    }
-    if (first_c < nb) {
-        for (long base = bnc[first_c]; base < tc; base += (long)E * g.n) {
-            double v[E];
-            UNR for (int e = 0; e < E; e++) {
-                const long q = base + g.tid + (long)e * g.n;
-                v[e] = 0;
-                if (q < tc) { const int r = block_of(bnc, first_c, q); v[e] = x.ac[boc[r] + (q - bnc[r])]; }
-            }
-            g.sync();
-            UNR for (int e = 0; e < E; e++) {
-                const long q = base + g.tid + (long)e * g.n;
-                if (q < tc) x.ac[q] = v[e];
-            }
-            g.sync();
-        }
-    }
-    for (int q = g.tid; q < MAX_SLOTS; q += g.n) {
-        if (key[q] < 0) continue;
-        x.H[q].hoff = bnh[rank[q]];
-        x.H[q].coff = bnc[crank[q]];
-    }
-    g.sync();
-}
-// before op pc: compact the LDS arena when fewer than nh hashes / nc coefficient rows are free
-// (every thread; the caller has synchronised, so every thread reads the same state); *used_h /
-// *used_c: the arena's use after the check, as every thread saw it. The barrier after the reads: a
-// thread-0 or wave-0 op allocates (moves hused) as soon as its thread passes here, and a wave still
-// reading the arena state would then decide differently (an unmatched compaction barrier).
-AI void arena_ensure(Ctx& x, int pc, long nh, long nc, long* used_h, long* used_c) {
-    const Arena& A = *x.A;
-    const long uh = A.hused, uc = A.cused;
-    const bool room = A.hcap - uh >= nh && A.ccap - uc >= nc;
-    x.g.sync();
-    if (room) {
-        *used_h = uh;
-        *used_c = uc;
-        return;
-    }
-    arena_compact(x, pc, used_h, used_c);
 }
 
 // output header finish (thread 0): pruned amount into both independent parts (PZsparse.cu:347-349)
@@ -1066,9 +857,7 @@ AI bool order_keys(Ctx& x, const Terms& T, int N, KeyBufs& K) {
 #endif
 
 // group sums in term order, keep flags and pruned amounts, compaction, output (keys ordered)
-// LA: the build can run on the LDS arena (reach_kernel<NT, true>, the host emulation); the HBM
-// kernels compile without its exact-size check (its inlined compaction would cost them registers)
-template <class Pol, bool LA = true>
+template <class Pol>
 AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, const KeyBufs& K) {
     const Grp& g = x.g;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1099,19 +888,8 @@ AI void simplify_groups(Ctx& x, int o, const Terms& T, const Pol& pol, int N, co
         kp[q] = keep;
     }
     g.sync();
-    // LDS arena: the room this output needs is known exactly once the keeps are counted. The arena
-    // state is read here, before the scan's barriers: nothing allocates until thread 0 does below.
-    // Pass 2 reads only the keys, the positions and the parked sums, not the sources, so the
-    // arena can be compacted after the scan (arena_compact keeps its tables in the stage).
-    long uh = 0, uc = 0;
-    if (LA && x.A->lds) { uh = x.A->hused; uc = x.A->cused; }
     PHASE(2)
     const int K_ = block_scan(x, kp, N);
-    if (LA && x.A->lds) {
-        if (!(x.A->hcap - uh >= K_ && x.A->ccap - uc >= (long)K_ * n)) arena_compact(x, x.pc, &uh, &uc);
-        x.bud_h = x.A->hcap - uh - K_;
-        x.bud_c = x.A->ccap - uc - (long)K_ * n;
-    }
     if (g.tid == 0) {
         arena_alloc_t0(x, x.H[o], K_, n);
         x.A->bytes += T.in_bytes() + (double)K_ * (8.0 + 8.0 * n);

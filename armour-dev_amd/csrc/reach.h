@@ -487,7 +487,6 @@ inline int* g_op_stats = nullptr;
 // host emulation: per op, the output handle's monomial hashes (structure studies)
 inline void (*g_hash_sink)(int pc, const uint64_t* h, int n) = nullptr;
 #endif
-template <bool LA = true>  // LA: may run on the LDS arena (see simplify_groups)
 AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int T, int t, const double* q0,
                     const double* qd0, const double* qdd0, const ReachOut& out, long j, JrsJoint* jrs,
                     double* scratch, unsigned long long* prof, double* dump = nullptr, const JrsJoint* jrs_in = nullptr) {
@@ -498,78 +497,17 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
     const bool stamp = (prof || x.phase) && tid == 0;
     long long c_end = stamp ? clock64() : 0;
 #endif
-    // every handle empty at the job's start: the LDS arena's compaction reads the handles its live
-    // masks name, and a slot named before its first definition (an operand field an op does not
-    // use counts as a read) must not carry what the previous kernel left in LDS
+    // every handle empty at the job's start: a slot named before its first definition (an operand
+    // field an op does not use) must not carry what the previous job or kernel left in LDS
     for (int k = x.g.tid; k < MAX_SLOTS; k += x.g.n) {
         x.H[k].cnt = 0;
         x.H[k].hoff = 0;
         x.H[k].coff = 0;
     }
     x.g.sync();
-    int prev_sync = 1;
-    // LDS arena: free room every thread knows to be there without reading the arena state (the
-    // last check's free room less the bounds of the ops since); uniform across the group
-    x.bud_h = 0;
-    x.bud_c = 0;
     for (int pc = 0; pc < nops; pc++) {
         const Op op = prog[pc];
         const int par = op.par > 1 ? op.par : 1;  // ops pc .. pc + par - 1 run as one group
-        x.pc = pc;
-        if (LA && x.A->lds) {
-            // LDS arena: room for the op's output (its term count bounds the monomials it keeps),
-            // compacting to the live values when short; at most half the arena is asked for, a
-            // larger output that does not fit flags ERR_ARENA (planner.hip reruns on the HBM arena).
-            // An op within the budget needs no check. A four-wave simplify checks its exact need
-            // itself, after counting its keeps (simplify_groups), and sets the budget; any other op
-            // whose bound exceeds the budget checks behind a barrier. An op that allocates more
-            // than its bound (beyond half the arena) is caught by the allocation's capacity test
-            // (ERR_ARENA).
-            long nh = 0, nc = 0;
-            // (rows per output monomial: the output's element count, from the operand shapes)
-            auto nel = [&](int q) { return x.H[q].R * x.H[q].C; };
-            switch (op.code) {
-                case OP_MUL: {
-                    const int na = nel(op.a), nbe = nel(op.b);
-                    nh = op_terms(x, op);
-                    nc = nh * (na == 1 ? nbe : (nbe == 1 ? na : x.H[op.a].R * x.H[op.b].C));
-                    break;
-                }
-                case OP_ADD: case OP_ADD1D: {
-                    const int na = nel(op.a), nbe = nel(op.b);
-                    nh = op_terms(x, op);
-                    nc = nh * (na > nbe ? na : nbe);
-                    break;
-                }
-                case OP_STACK3: case OP_CROSS_PP: case OP_CROSS_C: nh = op_terms(x, op); nc = 3 * nh; break;
-                case OP_MAKE1D: case OP_MAKEROT: case OP_MAKEBOX: case OP_CONST: case OP_TRANSPOSE:
-                    nh = 64L * par; nc = 576L * par; break;
-                default: break;
-            }
-            nh = nh < x.A->hcap / 2 ? nh : x.A->hcap / 2;
-            nc = nc < x.A->ccap / 2 ? nc : x.A->ccap / 2;
-            if (nh > 0 || nc > 0) {
-                const bool simp = op.code == OP_MUL || op.code == OP_ADD || op.code == OP_ADD1D ||
-                                  op.code == OP_STACK3 || op.code == OP_CROSS_PP;
-#if defined(__HIP_DEVICE_COMPILE__)
-                const bool wide = simp && (op_terms(x, op) > 64 || (x.mode & 1));  // the four-wave path
-#else
-                const bool wide = simp;
-#endif
-                if (!wide) {
-                    if (x.bud_h < nh || x.bud_c < nc) {
-                        if (!prev_sync) x.g.sync();
-                        long uh, uc;
-                        arena_ensure(x, pc, nh, nc, &uh, &uc);
-                        x.bud_h = x.A->hcap - uh;
-                        x.bud_c = x.A->ccap - uc;
-                    }
-                    x.bud_h -= nh;
-                    x.bud_c -= nc;
-                }
-            }
-        }
-        prev_sync = op.sync;
 #if defined(__HIP_DEVICE_COMPILE__)
         long long c0 = 0;
         if (stamp) {
@@ -697,10 +635,10 @@ AI void run_program(Ctx& x, const RobotParams& rp, const Op* prog, int nops, int
 #if defined(__HIP_DEVICE_COMPILE__)
                 if (x.phase && tid == 0) x.phase[1] += (unsigned long long)(clock64() - pt);
 #endif
-                if (cls == 0) simplify_groups<decltype(p1), LA>(x, op.o, Tm, p1, N, K);
-                else if (cls == 1) simplify_groups<decltype(p3), LA>(x, op.o, Tm, p3, N, K);
-                else if (cls == 2) simplify_groups<decltype(p9), LA>(x, op.o, Tm, p9, N, K);
-                else simplify_groups<decltype(pp), LA>(x, op.o, Tm, pp, N, K);
+                if (cls == 0) simplify_groups<decltype(p1)>(x, op.o, Tm, p1, N, K);
+                else if (cls == 1) simplify_groups<decltype(p3)>(x, op.o, Tm, p3, N, K);
+                else if (cls == 2) simplify_groups<decltype(p9)>(x, op.o, Tm, p9, N, K);
+                else simplify_groups<decltype(pp)>(x, op.o, Tm, pp, N, K);
                 break;
             }
         }
@@ -781,28 +719,6 @@ struct ProgramBuilder {
         }
     }
     void rel(std::initializer_list<int> l) { for (int s : l) rel(s); }
-    // Slots whose value is live at the start of each op (a backward pass over the tape; an op reads
-    // the slots among its a, b, c fields — fields that are constants for its code count as reads
-    // too, which only keeps more alive), two 64-bit words per op. The per-job engine's LDS arena
-    // compacts to exactly these values (pz_engine.h arena_compact).
-    std::vector<uint64_t> live_masks() const {
-        const int n = (int)ops.size();
-        std::vector<uint64_t> m(2 * (size_t)n, 0);
-        uint64_t l0 = 0, l1 = 0;
-        auto set = [&](int q) { if (q >= 0 && q < nslots) { if (q < 64) l0 |= 1ull << q; else l1 |= 1ull << (q - 64); } };
-        for (int pc = n - 1; pc >= 0; pc--) {
-            const Op& op = ops[pc];
-            if (op.o >= 0 && op.o < nslots) {
-                if (op.o < 64) l0 &= ~(1ull << op.o); else l1 &= ~(1ull << (op.o - 64));
-            }
-            set(op.a);
-            set(op.b);
-            set(op.c);
-            m[2 * pc] = l0;
-            m[2 * pc + 1] = l1;
-        }
-        return m;
-    }
     void emit(int code, int o = -1, int a = 0, int b = 0, int c = 0, int i = 0, double s = 0.0) {
         Op op;
         op.code = code; op.o = o; op.a = a; op.b = b; op.c = c; op.i = i; op.s = s; op.sync = 1; op.par = 0;

@@ -6,11 +6,9 @@
 // Two widths of the same kernel: 128 threads, four workgroups (eight waves) per CU, for batches
 // up to JOB_ENGINE_JOBS; 256 threads, two per CU, for batches that fit the chip in one round
 // (<= 2 x CUs jobs), where a job's latency is the reach time and the extra waves shorten the large
-// operators' passes. Both at the VGPR budget of two waves per SIMD. A third form for batches of at
-// most one job per CU (the drop-in's single plan): 256 threads whose arena lives in LDS (the rest
-// of the CU's 160 KB), compacted to the live values between ops (pz_engine.h arena_compact), so no
-// operator round-trips HBM for its operands or output; a job whose live values outgrow it flags
-// ERR_ARENA and the batch runs again on the HBM arena (planner.hip run_reach).
+// operators' passes. Both at the VGPR budget of two waves per SIMD. (Rounds 4-5 also carried a
+// third form whose arena lived in LDS, compacted to the live values between ops: bitwise the HBM
+// arena, but slower, 3.43 against 3.28 ms per single plan; removed in round 6)
 #include "reach.h"
 
 namespace armour {
@@ -31,11 +29,6 @@ constexpr int KEY_CAP_LDS = REACH_CFG_KEYS;
 constexpr int STAGE_DOUBLES = REACH_CFG_STAGE;
 constexpr int REACH_WG_PER_CU = REACH_CFG_WG_PER_CU;
 constexpr int POOL_DOUBLES = 1024;   // handle payloads (ProgramBuilder::slot_offsets)
-// the LDS arena of the one-job-per-CU form: with the 256-thread kernel's other LDS (~41 KB) it fills
-// the CU's 160 KB; the live values of a job peak near 35 KB (tests/emu: every job of the survey
-// sample fits this capacity bitwise, smaller ones flag ERR_ARENA)
-constexpr int LDS_ARENA_H = 2048;
-constexpr int LDS_ARENA_C = 13184;
 
 // The reach phase's counters: the algorithmic byte count, the capacity maxima occ[8] (arena
 // hashes, arena rows, operator terms, link / torque k-only monomials) and the per-world error
@@ -65,11 +58,21 @@ __device__ inline void zero_counters(const ReachCounters& c, int* err, int W) {
     if (threadIdx.x == 0 && c.pc_next) *c.pc_next = 0;
 }
 
+// The launch's execution span on the device clock (wall_clock64, s_memrealtime): the first
+// workgroup's start in occ[5] (as ~t, so that atomicMax keeps the earliest) and the last
+// workgroup's end in occ[6], published with the other counters (hsum[6], hsum[7]). This is the
+// quantity rocprofv3 --kernel-trace reports as the kernel's duration; HIP events around the launch
+// also count the time the kernel waits for CUs that other planners' kernels hold (bench.py's
+// roofline takes the span, armour_get_reach_span).
+__device__ inline void span_start(const ReachCounters& c) {
+    if (threadIdx.x == 0) atomicMax(&c.occ[5], ~(unsigned long long)wall_clock64());
+}
 // after a workgroup's last job: the last workgroup of the grid copies the counters out (reads
 // through device-scope atomics, so every other workgroup's updates are seen)
 __device__ inline void publish_counters(const ReachCounters& c, int* err, int W, int* last) {
     __syncthreads();
     if (threadIdx.x == 0) {
+        atomicMax(&c.occ[6], (unsigned long long)wall_clock64());
         __threadfence();
         *last = atomicAdd(c.done, 1u) == gridDim.x - 1;
     }
@@ -155,16 +158,11 @@ struct ReachArgs {
     int mode;                   // engine diagnostics (Ctx::mode)
     unsigned long long* phase;  // optional phase cycle totals [16] (null: off; exclusive with prof)
     double* dump;               // optional op-by-op state of job 0 (null: off)
-    const uint64_t* live;       // [nops][2] live slots at each op (ProgramBuilder::live_masks), LDS arena form
-    int lds_h, lds_c;           // the LDS arena's capacity in use (<= LDS_ARENA_H / _C; smaller for tests)
 };
 
-// 2 waves per SIMD: 256 registers per lane (VGPR + AGPR); NT threads per job; LA: the LDS arena (one
-// workgroup per CU: one wave per SIMD, 512 registers, no spills)
-template <int NT, bool LA = false>
-__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(LA ? 1 : REACH_CFG_WAVES_PER_SIMD, LA ? 1 : REACH_CFG_WAVES_PER_SIMD))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
-    __shared__ uint64_t lah[LA ? LDS_ARENA_H : 1];
-    __shared__ double lac[LA ? LDS_ARENA_C : 1];
+// 2 waves per SIMD: 256 registers per lane (VGPR + AGPR); NT threads per job
+template <int NT>
+__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(REACH_CFG_WAVES_PER_SIMD, REACH_CFG_WAVES_PER_SIMD))) void reach_kernel(const RobotParams* __restrict__ rpp, ReachArgs a, ReachOut out) {
     __shared__ PZH H[MAX_SLOTS];
     __shared__ double pool[POOL_DOUBLES + 9];  // + 9: header reads of a full 3x3 past a small slot
     __shared__ uint64_t kh[KEY_CAP_LDS];
@@ -181,20 +179,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     __shared__ unsigned long long phase_acc[16];
     __shared__ int last;
 
+    span_start(a.rc);
     const RobotParams& rp = *rpp;
     Ctx x;
     x.g = Grp{(int)threadIdx.x, (int)blockDim.x};
     x.H = H;
     x.pool = pool;
     x.A = &arena;
-    x.live = a.live;
-    if (LA) {
-        x.ah = lah;
-        x.ac = lac;
-    } else {
-        x.ah = a.arena_h + (long)blockIdx.x * a.arena_cap;
-        x.ac = a.arena_c + (long)blockIdx.x * a.arena_cap * 3;
-    }
+    x.ah = a.arena_h + (long)blockIdx.x * a.arena_cap;
+    x.ac = a.arena_c + (long)blockIdx.x * a.arena_cap * 3;
     for (int k = threadIdx.x; k < a.nslots; k += blockDim.x) H[k].off = a.slot_off[k];
     x.kh = kh; x.ki = ki; x.kp = kp; x.cap_lds = KEY_CAP_LDS;
     x.gkh = a.gkh + (long)blockIdx.x * a.gcap;
@@ -216,19 +209,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     for (long job = blockIdx.x; job < njobs; job += gridDim.x) {
         const int w = (int)(job / a.T), t = (int)(job % a.T);
         if (threadIdx.x == 0) {
-            if (LA) {
-                arena.hcap = a.lds_h;
-                arena.ccap = a.lds_c;
-                arena.lds = 1;
-            } else {
-                arena.hcap = a.arena_cap;
-                arena.ccap = a.arena_cap * 3;
-                arena.lds = 0;
-            }
+            arena.hcap = a.arena_cap;
+            arena.ccap = a.arena_cap * 3;
             arena.hused = 0;
             arena.cused = 0;
-            arena.ncompact = 0;
-            arena.cmoved = 0;
             arena.bytes = 0;
             err = 0;
         }
@@ -238,7 +222,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
             qdd0s[threadIdx.x] = a.qdd0[w * NF + threadIdx.x];
         }
         __syncthreads();
-        run_program<LA>(x, rp, a.prog, a.nops, a.T, t, q0s, qd0s, qdd0s, out, job, jrs, scratch, a.prof,
+        run_program(x, rp, a.prog, a.nops, a.T, t, q0s, qd0s, qdd0s, out, job, jrs, scratch, a.prof,
                     job == 0 ? a.dump : nullptr, a.jrs + job * NF);
         if (threadIdx.x == 0) {
             if (err) atomicOr(&out.err[w], err);

@@ -216,6 +216,11 @@ int armour_get_reach_profile(armour_planner* p, unsigned long long* cycles_terms
  * NaN; the solver never produces one). Returns ARMOUR_PC_COUNT; ARMOUR_E_STATE when the cache is off. */
 #define ARMOUR_PC_COUNT 7
 int armour_get_plane_cache_stats(armour_planner* p, long long* out, int n);
+/* Execution span of the last reach launch on the device clock (wall_clock64): from the first
+ * workgroup's start to the last workgroup's end, the duration rocprofv3 --kernel-trace reports
+ * for the kernel (the reach_kernel_ms of armour_timing, HIP events around the launch, also counts
+ * the time the launch waits for CUs held by other planners' kernels). Milliseconds. */
+int armour_get_reach_span(armour_planner* p, double* span_ms);
 /* op-by-op state of job 0 (world 0, t = 0) of the last reach: per op 8 doubles [monomial count,
  * block size, centre[0..2], nominal ind[0], interval ind[0], sum|m|[0]] of the op's output, when
  * ARMOUR_DUMP_OPS was set at armour_create; returns the op count. */

@@ -30,19 +30,6 @@ def set_robot(robot_struct=None):
     NJ = int(robot_struct.num_joints) if robot_struct is not None else 7
 
 
-def set_lds_arena(hcap=0, ccap=0):
-    """> 0: the following reach_job calls run on a compacting arena of this capacity (the per-job
-    engine's LDS arena, pz_engine.h arena_compact); 0: the bump arena"""
-    lib().emu_set_lds_arena(ctypes.c_long(hcap), ctypes.c_long(ccap))
-
-
-def compactions():
-    """(compactions, coefficient rows moved) of the last reach_job on the compacting arena"""
-    out = (ctypes.c_long * 2)()
-    lib().emu_compactions(out)
-    return out[0], out[1]
-
-
 def reach_job(world, T, t, fused=True):
     """Outputs of job (world, t) as the kernel writes them (fused: the program's cross products
     as single ops, else composed from views / products / differences / stack)."""

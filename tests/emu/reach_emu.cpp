@@ -11,10 +11,6 @@ using namespace armour;
 
 static double* g_dump = nullptr;
 static int g_unfused = 0;
-static long g_lds_h = 0, g_lds_c = 0;  // > 0: a compacting arena of this capacity (the device's LDS arena)
-extern "C" void emu_set_lds_arena(long hcap, long ccap) { g_lds_h = hcap; g_lds_c = ccap; }
-static long g_ncompact = 0, g_cmoved = 0;  // the last job's LDS-arena compactions, coefficient rows moved
-extern "C" void emu_compactions(long* out) { out[0] = g_ncompact; out[1] = g_cmoved; }
 extern "C" void emu_set_dump(double* d) { g_dump = d; }
 extern "C" void emu_set_unfused(int u) { g_unfused = u; }
 extern "C" void emu_set_stats(int* st) { armour::g_op_stats = st; }
@@ -67,13 +63,7 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     std::vector<int> kp(kcap);
     double red[18];
     int iscan[2];
-    Arena A{cap, cap * 3, 0, 0, 0.0, 0, 0, 0};
-    const std::vector<uint64_t> live = pb.live_masks();
-    if (g_lds_h > 0) {
-        A.hcap = g_lds_h;
-        A.ccap = g_lds_c;
-        A.lds = 1;
-    }
+    Arena A{cap, cap * 3, 0, 0, 0.0};
     int err = 0;
     Ctx x;
     x.g = Grp{0, 1};
@@ -82,7 +72,6 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     x.A = &A;
     x.ah = ah.data();
     x.ac = ac.data();
-    x.live = live.data();
     x.kh = kh.data(); x.ki = ki.data(); x.kp = kp.data(); x.cap_lds = kcap;
     x.gkh = kh.data(); x.gki = ki.data(); x.gkp = kp.data(); x.cap_glb = kcap;
     std::vector<double> gout(9 * (size_t)kcap);
@@ -108,9 +97,6 @@ extern "C" int emu_reach(int T, int t, const double* q0, const double* qd0, cons
     double scratch[2 * NF];
     run_program(x, rp, pb.ops.data(), (int)pb.ops.size(), T, t, q0, qd0, qdd0, out, 0, jrs, scratch, nullptr, g_dump);
     *arena_used = A.hused;
-    g_ncompact = A.ncompact;
-    g_cmoved = A.cmoved;
-    if (g_lds_h > 0 && err) *arena_used = -1;
     if (arena_bytes) *arena_bytes = A.bytes;
     if (nops) *nops = (int)pb.ops.size();
     if (nslots) *nslots = pb.nslots;

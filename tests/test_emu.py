@@ -89,35 +89,3 @@ def test_emulated_program_fetch_matches_oracle():
             np.testing.assert_allclose(o["torque_radius"], P.torque_radius()[t], rtol=0, atol=1e-12)
     finally:
         emu.set_robot(None)
-
-
-KEYS = ("link_gens", "link_center", "link_rad", "link_cnt", "link_hash", "link_coef", "tq_center", "tq_rad",
-        "tq_cnt", "tq_hash", "tq_coef", "torque_radius")
-
-
-def test_lds_arena_compaction_bitwise():
-    """The per-job engine's LDS arena (pz_engine.h arena_compact: the live values of
-    ProgramBuilder::live_masks moved to the bottom between ops, handles repointed) at the device's
-    capacity (reach_kernel.hip LDS_ARENA_H / _C) gives bitwise the outputs of the bump arena on
-    full-range jobs; at smaller capacities a job either matches bitwise or flags ERR_ARENA (the
-    planner then runs the batch on the HBM arena), never a silent difference"""
-    flagged = 0
-    try:
-        for seed in range(4):
-            world = make_world(200 + seed, 20, profile="survey")
-            for t in (0, 63, 99):
-                emu.set_lds_arena(0, 0)
-                a = emu.reach_job(world, 100, t)
-                assert a["err"] == 0 and a["arena"] > 2048  # the bump arena outgrows the LDS one
-                for cap, must_fit in (((2048, 13184), True), ((1000, 6500), False)):
-                    emu.set_lds_arena(*cap)
-                    b = emu.reach_job(world, 100, t)
-                    if b["err"]:
-                        assert not must_fit and b["err"] == 1, (seed, t, cap, b["err"])  # ERR_ARENA
-                        flagged += 1
-                        continue
-                    for k in KEYS:
-                        np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} seed {seed} t {t} cap {cap}")
-    finally:
-        emu.set_lds_arena(0, 0)
-    assert flagged > 0, "the small capacity never overflowed: the fallback path is untested"

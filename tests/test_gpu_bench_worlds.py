@@ -9,11 +9,11 @@ with the oracle's plan frozen in tests/golden/bench_survey_T100_O20.npz and its 
   * feasibility (finalize_solution, KPR/NLPclass.cu:422-538) and solver status identical for all
     3924 worlds;
   * the solver's path (iteration count, and k_opt within 1e-8 for a converged or feasible plan)
-    identical for at least 99 % of them; see the bar at the end. An infeasible plan writes -1
+    identical for at least 99.5 % of them; see the bar at the end. An infeasible plan writes -1
     (KPR/armour_main.cu:326-334), so its k_opt is not an output; its iterates run through nearly
     singular Newton systems that amplify rounding-level differences of g / J (DESIGN.md §2,
     profiles/r02_ipm_divergence.log), and it is held to identical status and feasibility (its
-    iteration count and k_opt difference are reported; it counts against the 1 % off-path bar).
+    iteration count and k_opt difference are reported; it counts against the 0.5 % off-path bar).
 """
 import os
 import threading
@@ -98,8 +98,7 @@ def test_bench_step_matches_oracle_world_by_world():
 
 def test_single_world_plans_match_oracle():
     """The drop-in's batch — one world per call — takes other paths than the bench step: the
-    per-job reach engine (reach_kernel<256>, the HBM arena by default; the LDS-arena form
-    reach_kernel<256, true> is opt-in, ARMOUR_LDS_ARENA=1), the sync-free tail from the
+    per-job reach engine (reach_kernel<256>), the sync-free tail from the
     second iteration, and restoration phases after the interior-point loop. The first 48 headline
     worlds planned one at a time against the same frozen oracle plans: every decision identical,
     and the solver's path (iterations, k_opt within 1e-8 when converged or feasible) for all but

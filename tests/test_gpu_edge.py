@@ -208,39 +208,6 @@ def test_sync_free_tail_matches_synchronised(tail, search):
             assert np.array_equal(planners[0].link_centers(w), planners[1].link_centers(w))
 
 
-@pytest.mark.parametrize("scale", ["1", "8"])
-def test_lds_arena_matches_hbm_arena(scale):
-    """The per-job engine's LDS arena (ARMOUR_LDS_ARENA=1: a single plan's jobs, one workgroup
-    each, on reach_kernel<256, true> with live-value compaction, pz_engine.h arena_compact) gives
-    bitwise the reach sets and plans of the HBM bump arena (the default), every time (each world
-    twice: a race between waves shows as a difference somewhere; round 4 found two this way); at an
-    eighth of the LDS capacity (ARMOUR_LDS_ARENA_SCALE=8) jobs overflow and the planner's rerun on
-    the HBM arena gives them too"""
-    import os
-
-    T, O = 100, 20
-    worlds = [[A.make_world(s, O, profile="survey")] for s in range(8)] + \
-             [[A.make_world(200 + s, O, profile="survey")] for s in range(4)]
-    base = A.Planner(T=T, max_obstacles=O, max_worlds=1)  # the HBM arena
-    os.environ["ARMOUR_LDS_ARENA"] = "1"
-    os.environ["ARMOUR_LDS_ARENA_SCALE"] = scale
-    try:
-        lds = A.Planner(T=T, max_obstacles=O, max_worlds=1)
-    finally:
-        del os.environ["ARMOUR_LDS_ARENA"]
-        del os.environ["ARMOUR_LDS_ARENA_SCALE"]
-    for w in worlds:
-        (b,), _ = base.plan(w)
-        for _ in range(2):
-            (a,), _ = lds.plan(w)
-            assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"]
-            assert (a["iterations"], a["evaluations"], a["status"]) == (b["iterations"], b["evaluations"], b["status"])
-            assert np.array_equal(lds.link_generators(0), base.link_generators(0))
-            assert np.array_equal(lds.torque_radius(0), base.torque_radius(0))
-            assert np.array_equal(lds.constraints(0), base.constraints(0))
-            assert np.array_equal(lds.link_centers(0), base.link_centers(0))
-
-
 @pytest.mark.parametrize("T", [10, 14])
 def test_short_horizon_plans_match_oracle(T):
     """Horizons shorter than the 2 NF + 1 = 15 extremum / cost tasks of a trial evaluation: the
