@@ -1732,7 +1732,11 @@ __device__ inline double mu_grid(double x) {
     return ldexp(gj, e - 1);
 }
 // A world kernel (one wave) works on its world's state staged in LDS: one coalesced round trip in
-// and one out, where lane 0's steps would otherwise wait on a dependent global load per field
+// and one out, where lane 0's steps would otherwise wait on a dependent global load per field. The
+// way out is taken only for a world the kernel works on (interior point: status 0 at entry;
+// restoration: WS_RESTO): an iteration's list may still name a world whose line search failed after
+// the list was formed, and that world's restoration phase can run concurrently on the planner's
+// second stream (planner.hip ipm_loop), so a copy of its state taken here must not be written back.
 __device__ inline void ws_copy(WorldState& dst, const WorldState& src) {
     static_assert(sizeof(WorldState) % 8 == 0, "WorldState in 8-byte words");
     const uint64_t* s = reinterpret_cast<const uint64_t*>(&src);
@@ -1744,9 +1748,10 @@ __global__ __launch_bounds__(64) void ipm_world_A(NlpDev d, int nside) {
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
     __syncthreads();
+    const bool act = S.status == 0;
     world_A_body(d, S, w, nside);
     __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (act) ws_copy(d.ws[w], S);
 }
 // pass A's world step: convergence test, barrier update, Newton step; every lane of the wave calls it
 __device__ inline void world_A_body(const NlpDev& d, WorldState& S, int w, int nside) {
@@ -1936,9 +1941,10 @@ __global__ __launch_bounds__(64) void ipm_world_B(NlpDev d) {
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
     __syncthreads();
+    const bool act = S.status == 0;
     world_B_body(d, S, w);
     __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (act) ws_copy(d.ws[w], S);
 }
 // the first trial's step alpha = S.ap as world_B_body forms it: pass B's block partials of the
 // primal fraction to the boundary, min onto 1 in block order (world_partials' arithmetic), for the
@@ -2062,9 +2068,10 @@ __global__ __launch_bounds__(64) void ipm_world_C(NlpDev d) {
     if (valid) {
         ws_copy(S, d.ws[w]);
         __syncthreads();
+        const bool act = S.status == 0;
         world_C_body(d, S, w);
         __syncthreads();
-        ws_copy(d.ws[w], S);
+        if (act) ws_copy(d.ws[w], S);
     }
     if (threadIdx.x != 0) return;
     if (valid && S.status == 0) {
@@ -2129,9 +2136,10 @@ __global__ __launch_bounds__(64) void ipm_world_Cs(NlpDev d) {
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
     __syncthreads();
+    const bool act = S.status == 0;
     world_Cs_body(d, S, blockIdx.x);
     __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (act) ws_copy(d.ws[w], S);
 }
 // The tail's whole line search in one round (planner.hip run_solver, sync-free tail): every trial
 // k = 0 .. max_ls - 1 of every running world was evaluated values-only (eval_trials_kernel with
@@ -2147,11 +2155,12 @@ __global__ __launch_bounds__(64) void ipm_world_Cs_all(NlpDev d) {
     if (valid) {
         ws_copy(S, d.ws[w]);
         __syncthreads();
+        const bool act = S.status == 0;
         if (d.b_in_cs) world_B_body(d, S, w);
         __syncthreads();  // lane 0's WorldState stores before every lane's reads (filter_pass)
         world_Cs_body(d, S, blockIdx.x);
         __syncthreads();
-        ws_copy(d.ws[w], S);
+        if (act) ws_copy(d.ws[w], S);
     }
     if (threadIdx.x != 0) return;
     if (valid && S.status == 0) {
@@ -2317,9 +2326,10 @@ __global__ __launch_bounds__(64) void ipm_world_D(NlpDev d) {
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
     __syncthreads();
+    const bool act = S.status == 0;
     world_D_body(d, S, w);
     __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (act) ws_copy(d.ws[w], S);
 }
 // the fused passes' world step: D's (of the previous iteration), then A's, one wave
 __global__ __launch_bounds__(64) void ipm_world_DA(NlpDev d, int nside) {
@@ -2328,11 +2338,12 @@ __global__ __launch_bounds__(64) void ipm_world_DA(NlpDev d, int nside) {
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
     __syncthreads();
+    const bool act = S.status == 0;
     world_D_body(d, S, w);
     __syncthreads();  // lane 0's WorldState stores before every lane's reads in world_A_body
     world_A_body(d, S, w, nside);
     __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (act) ws_copy(d.ws[w], S);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2503,7 +2514,8 @@ __global__ __launch_bounds__(64) void resto_world_G(NlpDev d) {
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
     __syncthreads();
-    if (S.status == WS_RESTO) {
+    const bool act = S.status == WS_RESTO;
+    if (act) {
         double P[NRG], init[NRG];
         int op[NRG];
 #pragma unroll
@@ -2520,7 +2532,7 @@ __global__ __launch_bounds__(64) void resto_world_G(NlpDev d) {
         }
     }
     __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (act) ws_copy(d.ws[w], S);
     if (threadIdx.x == 0 && d.rflag >= 0) resto_count(d, S.status == WS_RESTO, d.rflag);
 }
 
@@ -2553,7 +2565,8 @@ __global__ __launch_bounds__(64) void resto_world_V(NlpDev d) {
     __shared__ WorldState S;
     ws_copy(S, d.ws[w]);
     __syncthreads();
-    if (S.status == WS_RESTO && S.searching) {
+    const bool act = S.status == WS_RESTO;
+    if (act && S.searching) {
         double P[1];
         const double init[1] = {0.0};
         const int op[1] = {0};
@@ -2574,7 +2587,7 @@ __global__ __launch_bounds__(64) void resto_world_V(NlpDev d) {
         }
     }
     __syncthreads();
-    ws_copy(d.ws[w], S);
+    if (act) ws_copy(d.ws[w], S);
     if (threadIdx.x == 0) resto_count(d, S.status == WS_RESTO && S.searching, 1);
 }
 
@@ -2611,11 +2624,13 @@ __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
     const bool valid = !d.lcount || blockIdx.x < *d.lcount;
     const int i = blockIdx.x, w = valid ? d.wl[i] : 0;
     __shared__ WorldState S;
+    bool act = false;
     if (valid) {
         ws_copy(S, d.ws[w]);
         __syncthreads();
+        act = S.status == WS_RESTO;
     }
-    if (valid && S.status == WS_RESTO && S.searching) {
+    if (act && S.searching) {
         // trial k's sum on lane k, its blocks combined in order (world_partials_at's arithmetic)
         const int lane = threadIdx.x & 63;
         double v = 0.0;
@@ -2654,7 +2669,7 @@ __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
     }
     if (valid) {
         __syncthreads();
-        ws_copy(d.ws[w], S);
+        if (act) ws_copy(d.ws[w], S);
     }
     if (threadIdx.x != 0) return;
     if (d.rl_app) {  // inside the interior-point loop: the phase list, published by resto_publish
@@ -2675,8 +2690,9 @@ __global__ __launch_bounds__(64) void resto_world_Vs(NlpDev d) {
 
 // the phase list of the next phase iteration: the worlds appended since the last publish (failed
 // line searches, and the worlds the last phase iteration kept) moved from the append list `src` to
-// `dst`, its length into cnt[14] (the phase launches' lcount); the append list starts empty again
-__global__ __launch_bounds__(256) void resto_publish(NlpDev d, const int* src, int* dst) {
+// `dst`, its length into cnt[14] (the phase launches' lcount) and, for the host, into the mapped
+// flag `pflag` (null: none); the append list starts empty again
+__global__ __launch_bounds__(256) void resto_publish(NlpDev d, const int* src, int* dst, int* pflag) {
     __shared__ unsigned n;
     if (threadIdx.x == 0) n = atomicAdd(&d.cnt[12], 0u);
     __syncthreads();
@@ -2685,6 +2701,7 @@ __global__ __launch_bounds__(256) void resto_publish(NlpDev d, const int* src, i
     if (threadIdx.x == 0) {
         d.cnt[14] = n;
         d.cnt[12] = 0;
+        if (pflag) *pflag = (int)n;
     }
 }
 

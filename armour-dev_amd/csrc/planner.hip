@@ -115,6 +115,15 @@ struct armour_planner {
     bool spec_all = true;     // the sync-free tail's one-round line search (eval_trials_all, ipm_world_Cs_all)
     bool resto_spec = false;  // the restoration phase's one-round search (eval_trials_all, resto_world_Vs)
     bool resto_inline = true; // restoration phases inside the interior-point loop (ARMOUR_RESTO_INLINE=0: after it)
+    // In the sync-free tail the inline restoration phase runs on a second stream, concurrently with
+    // the next interior-point iteration (ARMOUR_RESTO_CONCURRENT=0: on the solver stream): its worlds
+    // are others than the interior point's, and its speculative rows start after the tail's
+    // (resto_soff rows into gs / fs / partial_s), so only the append list RL is shared; ipm_loop
+    // orders its publication (ev_ip, ev_pub) and joins the streams at the loop's end (ev_rend)
+    bool resto_conc = false;
+    hipStream_t rstream2 = nullptr;
+    hipEvent_t ev_ip = nullptr, ev_pub = nullptr, ev_rend = nullptr;
+    size_t resto_soff = 0;
     int tail_search = 1;      // its use (ARMOUR_TAIL_SEARCH): 0 rounds only, 1 adaptive, 2 always
     WorldState* h_ws = nullptr;
     double* h_f = nullptr;
@@ -455,7 +464,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         return rc;
     // the solver's two continue flags live in mapped host memory: kernels store 1 into them, the
     // host clears and reads them between synchronised rounds (no fill or copy per round)
-    HIPCK(hipHostMalloc((void**)&p->h_flags, 8 * sizeof(int), hipHostMallocMapped));
+    HIPCK(hipHostMalloc((void**)&p->h_flags, 12 * sizeof(int), hipHostMallocMapped));
     HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
     // active-world lists: two per iteration (ping-pong), two per line-search round
     // (+ two for the restoration phases inside the interior-point loop)
@@ -498,9 +507,21 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     p->resto_spec = p->spec && d.opt.resto_max > 0 && d.opt.max_ls <= EV_MAXK + 1 && d.opt.max_ls * NJ * Om <= UB_FULL &&
                     !std::getenv("ARMOUR_RESTO_ROUNDS");
     p->resto_inline = p->resto_spec && !(std::getenv("ARMOUR_RESTO_INLINE") && std::atoi(std::getenv("ARMOUR_RESTO_INLINE")) == 0);
+    p->resto_conc = p->resto_inline && p->spec_all && p->tail_worlds > 0 &&
+                    !(std::getenv("ARMOUR_RESTO_CONCURRENT") && std::atoi(std::getenv("ARMOUR_RESTO_CONCURRENT")) == 0);
+    if (p->resto_conc) {
+        HIPCK(hipStreamCreateWithFlags(&p->rstream2, hipStreamNonBlocking));
+        HIPCK(hipEventCreateWithFlags(&p->ev_ip, hipEventDisableTiming));
+        HIPCK(hipEventCreateWithFlags(&p->ev_pub, hipEventDisableTiming));
+        HIPCK(hipEventCreateWithFlags(&p->ev_rend, hipEventDisableTiming));
+    }
     if (p->spec) {
+        // rows of the speculative slots: the interior point's rounds use the first Wm x K (the
+        // sync-free tail's one-round search the first nall); a restoration phase Wm x max_ls, after
+        // the tail's rows when it runs concurrently with the tail (resto_soff)
         const size_t nall = p->spec_all ? (size_t)std::min(Wm, std::max(p->tail_worlds, 0)) * (d.K + 1) : 0;
-        const size_t nres = p->resto_spec ? (size_t)Wm * d.opt.max_ls : 0;
+        p->resto_soff = p->resto_conc ? nall : 0;
+        const size_t nres = p->resto_spec ? (size_t)Wm * d.opt.max_ls + p->resto_soff : 0;
         const size_t ns = std::max(std::max((size_t)Wm * d.K, nall), nres);
         if ((rc = p->alloc(&d.gs, ns * mmax)) || (rc = p->alloc(&d.fs, ns)) || (rc = p->alloc(&d.partial_s, ns * nblk_max * KA)))
             return rc;
@@ -793,16 +814,17 @@ static int nside_count(const armour_planner* p) {
 static bool eval_small_fits(const armour_planner* p) {
     return !p->eval_full && !p->armtd && !p->eval_f32 && p->mono_max[0] <= LM_S && p->mono_max[1] <= UM_S;
 }
-static void launch_eval(armour_planner* p, dim3 grid, const NlpDev& d, int mode, bool cached = true) {
+static void launch_eval(armour_planner* p, dim3 grid, const NlpDev& d, int mode, bool cached = true, hipStream_t s = nullptr) {
+    if (!s) s = p->stream;
     const bool c = cached && d.pcready && d.O > 0;
     if (c && eval_small_fits(p) && eval_pair_doubles(p->NJ * d.O) <= UB_S) {
-        hipLaunchKernelGGL(eval_kernel_small, grid, dim3(EVAL_THREADS), 0, p->stream, d, mode);
+        hipLaunchKernelGGL(eval_kernel_small, grid, dim3(EVAL_THREADS), 0, s, d, mode);
         return;
     }
     auto k = p->eval_f32 ? (d.armtd ? eval_kernel_t<float, true, false> : eval_kernel_t<float, false, false>)
                          : c ? (d.armtd ? eval_kernel_t<double, true, true> : eval_kernel_t<double, false, true>)
                              : (d.armtd ? eval_kernel_t<double, true, false> : eval_kernel_t<double, false, false>);
-    hipLaunchKernelGGL(k, grid, dim3(EVAL_THREADS), 0, p->stream, d, mode);
+    hipLaunchKernelGGL(k, grid, dim3(EVAL_THREADS), 0, s, d, mode);
 }
 
 // The interior-point loop over the nrun worlds listed in the first iteration list (d_lists[0..]):
@@ -835,9 +857,39 @@ static int ipm_loop(armour_planner* p, int nrun) {
     int ub = 0;          // an upper bound of the list's length now: the last phase grid, plus every
                          // interior-point world launched since (each could have failed)
     if (inl) HIPCK(hipMemsetAsync(d.cnt + 12, 0, sizeof(unsigned), p->stream));
-    auto resto_iter = [&](int bound) {
-        if (!inl || bound <= 0) return;
-        hipLaunchKernelGGL(resto_publish, dim3(1), dim3(256), 0, p->stream, d, (const int*)RL, PL);
+    // conc: this phase iteration runs on the second stream, concurrently with the next
+    // interior-point iteration (sync-free tail, p->resto_conc). The phase's worlds are not the
+    // interior point's (an iteration's list may still name a world that failed after the list was
+    // formed: the world kernels write back only the worlds they work on, nlp_kernels.hip ws_copy),
+    // and its speculative rows start resto_soff rows in (after the tail's); the
+    // one shared structure is the append list RL (cnt[12]): interior-point failures and the phase's
+    // kept worlds append to it with atomics, and resto_publish moves it to the phase list. So the
+    // publish waits for the interior-point iteration that appended (ev_ip), and the next
+    // interior-point iteration waits for the publish (ev_pub), not for the phase iteration. An
+    // interior-point iteration's snapshot of the list (pend_flag) may then miss the worlds the
+    // concurrent phase iteration keeps, so the host also reads the length each publish moved
+    // (flags[8 + (it & 1)], pub_known): a phase iteration that had worlds is followed by another at
+    // most two iterations later, as long as the loop runs.
+    bool conc_used = false;
+    bool pub_launched[2] = {false, false};
+    int pub_known = 0;
+    auto resto_iter = [&](int it, int bound, bool conc) -> int {
+        pub_launched[it & 1] = false;
+        if (!inl || bound <= 0) return 0;
+        hipStream_t s = p->stream;
+        if (conc) {
+            s = p->rstream2;
+            HIPCK(hipEventRecord(p->ev_ip, p->stream));
+            HIPCK(hipStreamWaitEvent(s, p->ev_ip, 0));
+            conc_used = true;
+        }
+        hipLaunchKernelGGL(resto_publish, dim3(1), dim3(256), 0, s, d, (const int*)RL, PL,
+                           conc ? d.flags + 8 + (it & 1) : nullptr);
+        pub_launched[it & 1] = conc;
+        if (conc) {
+            HIPCK(hipEventRecord(p->ev_pub, s));
+            HIPCK(hipStreamWaitEvent(p->stream, p->ev_pub, 0));
+        }
         const int nb = std::min(W0, bound);
         ub = nb;  // the phase keeps at most the worlds it took
         NlpDev dr = d;
@@ -849,12 +901,18 @@ static int ipm_loop(armour_planner* p, int nrun) {
         dr.lcount = d.cnt + 14;
         dr.rl_app = RL;
         dr.pend_flag = nullptr;
-        hipLaunchKernelGGL(resto_rows_G, dim3(d.nblk, nb), dim3(ROW_THREADS), 0, p->stream, dr);
-        hipLaunchKernelGGL(resto_world_G, dim3(nb), dim3(64), 0, p->stream, dr);
-        hipLaunchKernelGGL(eval_trials_all, dim3(p->T, nb), dim3(EVAL_THREADS), 0, p->stream, dr);
-        hipLaunchKernelGGL(resto_rows_Vs, dim3(d.nblk, nb * dr.K), dim3(ROW_THREADS), 0, p->stream, dr);
-        hipLaunchKernelGGL(resto_world_Vs, dim3(nb), dim3(64), 0, p->stream, dr);
-        launch_eval(p, dim3(p->T, nb), dr, 5);
+        if (conc) {
+            dr.gs = d.gs + p->resto_soff * (size_t)d.m;
+            dr.fs = d.fs + p->resto_soff;
+            dr.partial_s = d.partial_s + p->resto_soff * (size_t)d.nblk * KA;
+        }
+        hipLaunchKernelGGL(resto_rows_G, dim3(d.nblk, nb), dim3(ROW_THREADS), 0, s, dr);
+        hipLaunchKernelGGL(resto_world_G, dim3(nb), dim3(64), 0, s, dr);
+        hipLaunchKernelGGL(eval_trials_all, dim3(p->T, nb), dim3(EVAL_THREADS), 0, s, dr);
+        hipLaunchKernelGGL(resto_rows_Vs, dim3(d.nblk, nb * dr.K), dim3(ROW_THREADS), 0, s, dr);
+        hipLaunchKernelGGL(resto_world_Vs, dim3(nb), dim3(64), 0, s, dr);
+        launch_eval(p, dim3(p->T, nb), dr, 5, true, s);
+        return 0;
     };
     // Launches cover the active worlds only (NlpDev::wl): every line-search round's ipm_world_C
     // compacts the worlds still running / still searching into the next lists and publishes the
@@ -917,13 +975,14 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_world_Cs_all, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
             ub = std::min(W0, ub + nrun);
-            resto_iter(pend_known > 0 ? ub : 0);
+            if (int rc = resto_iter(it, pend_known > 0 || pub_known > 0 ? ub : 0, p->resto_conc)) return rc;
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
             if (tail) {
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
                 if (inl) pend_known = flr[6 + ((it - 1) & 1)];
+                pub_known = pub_launched[(it - 1) & 1] ? flr[8 + ((it - 1) & 1)] : 0;
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;
@@ -975,7 +1034,7 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_world_Cs, dim3(nrun), dim3(64), 0, p->stream, ds);
             launch_eval(p, dim3(p->T, nrun), ds, 5);
             ub = std::min(W0, ub + nrun);
-            resto_iter(pend_known > 0 ? ub : 0);
+            if (int rc = resto_iter(it, pend_known > 0 || pub_known > 0 ? ub : 0, p->resto_conc)) return rc;
             HIPCK(hipEventRecord(p->tev[it & 1], p->stream));
             HIPCK(hipGetLastError());
             cur = 1 - cur;
@@ -983,6 +1042,7 @@ static int ipm_loop(armour_planner* p, int nrun) {
                 // iteration it - 1's running count: the worlds iteration it was launched for
                 HIPCK(hipEventSynchronize(p->tev[(it - 1) & 1]));
                 if (inl) pend_known = flr[6 + ((it - 1) & 1)];
+                pub_known = pub_launched[(it - 1) & 1] ? flr[8 + ((it - 1) & 1)] : 0;
                 const int prev = ((volatile int*)p->h_flags)[2 + ((it - 1) & 1)];
                 backtracked = ((volatile int*)p->h_flags)[4 + ((it - 1) & 1)];
                 if (prev == 0) break;  // iteration it had nothing to do
@@ -1019,11 +1079,15 @@ static int ipm_loop(armour_planner* p, int nrun) {
         // (the phase list's bound: its length after round 0, plus the worlds that searched past
         // round 0 and so could have failed)
         if (inl) ub = std::min(W0, pend_known + nsearch);
-        resto_iter(ub);
+        if (int rc = resto_iter(it, ub, false)) return rc;
         if (nnext == 0) break;  // every world converged, hit the cap, failed or is in a restoration phase
         HIPCK(hipGetLastError());
         cur = 1 - cur;
         nrun = nnext;
+    }
+    if (conc_used) {  // the last phase iteration, before anything reads its worlds or reuses PL
+        HIPCK(hipEventRecord(p->ev_rend, p->rstream2));
+        HIPCK(hipStreamWaitEvent(p->stream, p->ev_rend, 0));
     }
     d.rl_app = nullptr;
     d.pend_flag = nullptr;
@@ -1287,6 +1351,10 @@ void armour_destroy(armour_planner* p) {
     if (p->stream) {
         for (int i = 0; i < 6; i++) (void)hipEventDestroy(p->ev[i]);
         for (int i = 0; i < 2; i++) (void)hipEventDestroy(p->tev[i]);
+        if (p->rstream2) (void)hipStreamSynchronize(p->rstream2);
+        for (hipEvent_t e : {p->ev_ip, p->ev_pub, p->ev_rend})
+            if (e) (void)hipEventDestroy(e);
+        if (p->rstream2) (void)hipStreamDestroy(p->rstream2);
         if (p->rstream && p->rstream != p->stream) (void)hipStreamDestroy(p->rstream);
         (void)hipStreamDestroy(p->stream);
     }

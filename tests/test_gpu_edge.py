@@ -153,6 +153,35 @@ def test_restoration_one_round_matches_rounds(variant, case):
         assert np.array_equal(g_s[w], Q.constraints(w))
 
 
+@pytest.mark.parametrize("tail", ["16", "1000"])
+def test_concurrent_restoration_matches_serial(tail):
+    """Restoration phase iterations inside the sync-free tail run on the planner's second stream,
+    concurrently with the next interior-point iteration (planner.hip ipm_loop, resto_conc, the
+    default): bitwise the plans of phase iterations in order on the planner's stream
+    (ARMOUR_RESTO_CONCURRENT=0). "1000" puts every iteration after the first in the tail, so most
+    phase iterations overlap an interior-point iteration."""
+    import os
+
+    T, O = 40, 10
+    worlds = [A.make_world(s, O, profile="survey") for s in range(64)]
+    planners = []
+    for conc in ("1", "0"):
+        os.environ["ARMOUR_TAIL_WORLDS"] = tail
+        os.environ["ARMOUR_RESTO_CONCURRENT"] = conc
+        try:
+            planners.append(A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds)))
+        finally:
+            del os.environ["ARMOUR_TAIL_WORLDS"]
+            del os.environ["ARMOUR_RESTO_CONCURRENT"]
+    (res_c, _), (res_s, _) = [P.plan(worlds) for P in planners]
+    assert sum(r["status"] == 4 for r in res_s) >= 8, "too few worlds in the restoration phase"
+    for w, (a, b) in enumerate(zip(res_c, res_s)):
+        assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"]
+        assert (a["iterations"], a["evaluations"], a["status"], a["feasible"], a["error"]) == \
+            (b["iterations"], b["evaluations"], b["status"], b["feasible"], b["error"]), w
+        assert np.array_equal(planners[0].constraints(w), planners[1].constraints(w))
+
+
 def test_inline_restart_after_other_worlds_finish():
     """A world whose restoration phase restarts the interior point inside ipm_loop (status
     WS_RESTART) while another world is still iterating, after which that other world converges and
