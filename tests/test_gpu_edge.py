@@ -254,3 +254,18 @@ def test_short_horizon_plans_match_oracle(T):
         assert abs(r["iterations"] - ro["iterations"]) <= it_tol, (w, r["iterations"], ro["iterations"])
         if r["status"] == 0 or r["feasible"]:
             np.testing.assert_allclose(r["k_opt"], ro["k_opt"], rtol=0, atol=1e-8)
+
+
+@pytest.mark.parametrize("W", [1, 64])
+def test_reach_span_on_the_device_clock(W):
+    """armour_get_reach_span: the last reach launch's execution span on the device clock (first
+    workgroup start to last workgroup end), for the per-job engine (one world) and the bundle engine
+    (64 worlds, 6400 jobs): positive, and within the reach phase's host-timed wall time."""
+    T, O = 100, 20
+    P = A.Planner(T=T, max_obstacles=O, max_worlds=W)
+    worlds = [A.make_world(s, O, profile="survey") for s in range(W)]
+    for _ in range(2):
+        tm = P.reach(worlds)
+    span = P.reach_span_ms()
+    assert span == tm["reach_span_ms"]
+    assert 0.0 < span <= tm["reach_ms"] + 0.05, (span, tm)
