@@ -1473,9 +1473,10 @@ struct AAcc {
     }
 };
 // pass A's row accumulation with the row's slacks and multipliers given (registers)
+template <int ML = 0>
 __device__ inline __attribute__((always_inline)) void row_A_sz(const NlpDev& d, long i, double v, const double* a, double L,
                                                                double U, double mu, double slo, double zlo, double shi,
-                                                               double zhi, AAcc& c) {
+                                                               double zhi, AAcc& c, double* ml = nullptr) {
     double wr = 0, sig = 0, c1 = 0, c2 = 0;
     if (has_lo(d, L)) {
         const double s = slo, z = zlo;
@@ -1514,7 +1515,10 @@ __device__ inline __attribute__((always_inline)) void row_A_sz(const NlpDev& d, 
         c.u1[p] += a[p] * c1;
         c.u2[p] += a[p] * c2;
 #pragma unroll
-        for (int q = p; q < NF; q++) c.M[k++] += sig * a[p] * a[q];
+        for (int q = p; q < NF; q++, k++) {
+            if (k < ML) ml[k * ROW_THREADS] += sig * a[p] * a[q];
+            else c.M[k] += sig * a[p] * a[q];
+        }
     }
 }
 __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, long i, double v, const double* a, double L,
@@ -1523,7 +1527,8 @@ __device__ inline __attribute__((always_inline)) void row_A(const NlpDev& d, lon
 }
 constexpr int NA = 55;  // pass A's partial sums per row block (<= KA)
 static_assert(NA <= KA, "pass A partials fit the partial slots");
-__device__ inline void reduce_A(const NlpDev& d, int w, AAcc& c, double* lds) {
+template <int ML = 0>
+__device__ inline void reduce_A(const NlpDev& d, int w, AAcc& c, double* lds, const double* ml = nullptr) {
     double* out = d.partial + ((long)w * d.nblk + blockIdx.x) * KA;
     double v[NA];
     int kinds[NA];
@@ -1531,7 +1536,7 @@ __device__ inline void reduce_A(const NlpDev& d, int w, AAcc& c, double* lds) {
     for (int j = 0; j < NF; j++) { v[j] = c.rdp[j]; v[39 + j] = c.u1[j]; v[46 + j] = c.u2[j]; }
     v[7] = c.inf_p; v[8] = c.compl0; v[9] = c.cm; v[10] = c.sumz;
 #pragma unroll
-    for (int k = 0; k < 28; k++) v[11 + k] = c.M[k];
+    for (int k = 0; k < 28; k++) v[11 + k] = k < ML ? ml[k * ROW_THREADS] : c.M[k];
     v[53] = c.sumc; v[54] = c.minc;
 #pragma unroll
     for (int k = 0; k < NA; k++) kinds[k] = (k >= 7 && k <= 9) ? 1 : k == 54 ? 2 : 0;
@@ -1590,12 +1595,26 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
 // passes D (of the previous iteration) and A (of this one) in one sweep over the rows: the trial
 // point D accepts is the point A works at, so each row's value and gradient are read once; the
 // arithmetic of ipm_rows_D then ipm_rows_A. D's sums go to partial2, A's to partial.
-__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
+// ML > 0 (ipm_rows_DA_lds, the wide launches): the first ML of pass A's 28 Newton-matrix
+// accumulators live in LDS, one slot per thread, with the same additions in the same order, so the
+// kernel holds 152 VGPRs instead of 216 and runs three waves per SIMD instead of two: a 1308-world
+// launch 790 -> 710 us, but a small grid's latency 17.2 -> 19.9 us (the slots' LDS round trips), so
+// the tail keeps the register form (planner.hip launch_rows_DA)
+constexpr int DA_ML = 20;
+template <int ML>
+__device__ __attribute__((always_inline)) void rows_DA_body(const NlpDev& d) {
     if (d.lcount && blockIdx.y >= *d.lcount) return;
     const int w = world_of(d, blockIdx.y);
     const WorldState& S = d.ws[w];
     if (S.status != 0) return;
     __shared__ double lds[(ROW_THREADS / 64) * NA];
+    double* ml = nullptr;
+    if constexpr (ML > 0) {
+        __shared__ double mls[ML * ROW_THREADS];
+        ml = mls + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < ML; k++) ml[k * ROW_THREADS] = 0.0;
+    }
     const double mu = S.mu, ad = S.ad, alpha = S.alpha;
     double wn[NF];
 #pragma unroll
@@ -1633,13 +1652,16 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) {
         }
 #pragma unroll
         for (int j = 0; j < NF; j++) wn[j] += wv * a[j];
-        row_A_sz(d, i, v, a, L, U, mu, sl, zl, sh, zh, c);
+        row_A_sz<ML>(d, i, v, a, L, U, mu, sl, zl, sh, zh, c, ml);
+        if constexpr (ML > 0) __asm__ volatile("" ::: "memory");  // the slots stay in LDS across rows
     }
     const int kinds[NF] = {};
     block_reduce_n(wn, kinds, lds, d.partial2 + ((long)w * d.nblk + blockIdx.x) * KA2);
     __syncthreads();
-    reduce_A(d, w, c, lds);
+    reduce_A<ML>(d, w, c, lds, ml);
 }
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA(NlpDev d) { rows_DA_body<0>(d); }
+__global__ __launch_bounds__(ROW_THREADS) void ipm_rows_DA_lds(NlpDev d) { rows_DA_body<DA_ML>(d); }
 
 __device__ bool chol_solve7(const double* M, double shift, const double* b, double* x) {
     double L[NF * NF];

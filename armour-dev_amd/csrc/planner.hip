@@ -120,6 +120,7 @@ struct armour_planner {
     // are others than the interior point's, and its speculative rows start after the tail's
     // (resto_soff rows into gs / fs / partial_s), so only the append list RL is shared; ipm_loop
     // orders its publication (ev_ip, ev_pub) and joins the streams at the loop's end (ev_rend)
+    bool da_lds = true;       // wide grids take ipm_rows_DA_lds (ARMOUR_DA_REGS=1: the register form)
     bool resto_conc = false;
     hipStream_t rstream2 = nullptr;
     hipEvent_t ev_ip = nullptr, ev_pub = nullptr, ev_rend = nullptr;
@@ -218,6 +219,7 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
     for (int i = 0; i < 6; i++) HIPCK(hipEventCreate(&p->ev[i]));
     for (int i = 0; i < 2; i++) HIPCK(hipEventCreateWithFlags(&p->tev[i], hipEventDisableTiming));
     if (const char* e = std::getenv("ARMOUR_TAIL_WORLDS")) p->tail_worlds = std::atoi(e);
+    p->da_lds = !std::getenv("ARMOUR_DA_REGS");
     if (const char* e = std::getenv("ARMOUR_TAIL_SEARCH"))
         p->tail_search = !std::strcmp(e, "rounds") ? 0 : !std::strcmp(e, "one") ? 2 : 1;
     const int T = p->T, NJ = p->NJ, Om = p->Omax > 0 ? p->Omax : 1, Wm = p->Wmax;
@@ -948,7 +950,9 @@ static int ipm_loop(armour_planner* p, int nrun) {
             hipLaunchKernelGGL(ipm_rows_A, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
             hipLaunchKernelGGL(ipm_world_A, dim3(nrun), dim3(64), 0, p->stream, di, ns);
         } else {
-            hipLaunchKernelGGL(ipm_rows_DA, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
+            // the LDS-accumulator form for grids of several blocks per CU (nlp_kernels.hip rows_DA_body)
+            const bool wide = p->da_lds && (long)d.nblk * nrun >= 4L * p->ncu;
+            hipLaunchKernelGGL(wide ? ipm_rows_DA_lds : ipm_rows_DA, dim3(d.nblk, nrun), dim3(ROW_THREADS), 0, p->stream, di);
             hipLaunchKernelGGL(ipm_world_DA, dim3(nrun), dim3(64), 0, p->stream, di, ns);
         }
         const bool one = tl && p->spec_all && (p->tail_search == 2 || backtracked > 0);

@@ -269,3 +269,28 @@ def test_reach_span_on_the_device_clock(W):
     span = P.reach_span_ms()
     assert span == tm["reach_span_ms"]
     assert 0.0 < span <= tm["reach_ms"] + 0.05, (span, tm)
+
+
+def test_row_pass_lds_accumulators_match_registers():
+    """The fused row pass's wide-grid form (ipm_rows_DA_lds: the first 20 of pass A's Newton-matrix
+    accumulators in LDS, one slot per thread, three waves per SIMD; launched when the grid holds at
+    least four blocks per CU) gives bitwise the plans of the register form (ARMOUR_DA_REGS=1): 96
+    headline worlds, 15 row blocks each, so the early iterations take the LDS form."""
+    import os
+
+    T, O = 100, 20
+    worlds = [A.make_world(s, O, profile="survey") for s in range(96)]
+    planners = []
+    for regs in (False, True):
+        if regs:
+            os.environ["ARMOUR_DA_REGS"] = "1"
+        try:
+            planners.append(A.Planner(T=T, max_obstacles=O, max_worlds=len(worlds)))
+        finally:
+            os.environ.pop("ARMOUR_DA_REGS", None)
+    (res_l, _), (res_r, _) = [P.plan(worlds) for P in planners]
+    for w, (a, b) in enumerate(zip(res_l, res_r)):
+        assert np.array_equal(a["k_opt"], b["k_opt"]) and a["cost"] == b["cost"], w
+        assert (a["iterations"], a["evaluations"], a["status"], a["feasible"]) == \
+            (b["iterations"], b["evaluations"], b["status"], b["feasible"]), w
+        assert np.array_equal(planners[0].constraints(w), planners[1].constraints(w))
