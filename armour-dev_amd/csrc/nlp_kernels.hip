@@ -1597,9 +1597,9 @@ __global__ __launch_bounds__(ROW_THREADS) void ipm_rows_A(NlpDev d) {
 // arithmetic of ipm_rows_D then ipm_rows_A. D's sums go to partial2, A's to partial.
 // ML > 0 (ipm_rows_DA_lds, the wide launches): the first ML of pass A's 28 Newton-matrix
 // accumulators live in LDS, one slot per thread, with the same additions in the same order, so the
-// kernel holds 152 VGPRs instead of 216 and runs three waves per SIMD instead of two: a 1308-world
-// launch 790 -> 710 us, but a small grid's latency 17.2 -> 19.9 us (the slots' LDS round trips), so
-// the tail keeps the register form (planner.hip launch_rows_DA)
+// kernel holds 166 VGPRs instead of 216 and runs three waves per SIMD instead of two: a 1308-world
+// launch 744 -> 651 us, but a small grid's latency 17.2 -> 19.9 us (the slots' LDS round trips), so
+// grids below four blocks per CU keep the register form (planner.hip ipm_loop)
 constexpr int DA_ML = 20;
 template <int ML>
 __device__ __attribute__((always_inline)) void rows_DA_body(const NlpDev& d) {

@@ -115,12 +115,12 @@ struct armour_planner {
     bool spec_all = true;     // the sync-free tail's one-round line search (eval_trials_all, ipm_world_Cs_all)
     bool resto_spec = false;  // the restoration phase's one-round search (eval_trials_all, resto_world_Vs)
     bool resto_inline = true; // restoration phases inside the interior-point loop (ARMOUR_RESTO_INLINE=0: after it)
+    bool da_lds = true;       // wide grids take ipm_rows_DA_lds (ARMOUR_DA_REGS=1: the register form)
     // In the sync-free tail the inline restoration phase runs on a second stream, concurrently with
     // the next interior-point iteration (ARMOUR_RESTO_CONCURRENT=0: on the solver stream): its worlds
     // are others than the interior point's, and its speculative rows start after the tail's
     // (resto_soff rows into gs / fs / partial_s), so only the append list RL is shared; ipm_loop
     // orders its publication (ev_ip, ev_pub) and joins the streams at the loop's end (ev_rend)
-    bool da_lds = true;       // wide grids take ipm_rows_DA_lds (ARMOUR_DA_REGS=1: the register form)
     bool resto_conc = false;
     hipStream_t rstream2 = nullptr;
     hipEvent_t ev_ip = nullptr, ev_pub = nullptr, ev_rend = nullptr;
@@ -464,8 +464,10 @@ static int planner_init(armour_planner* p, const armour_config* cfg, const armou
         (rc = p->alloc(&d.ws, (size_t)Wm)) ||
         (rc = p->alloc(&p->feas, (size_t)Wm)))
         return rc;
-    // the solver's two continue flags live in mapped host memory: kernels store 1 into them, the
-    // host clears and reads them between synchronised rounds (no fill or copy per round)
+    // the solver's counts for the host live in mapped host memory (NlpDev::flags: [0, 1] a round's
+    // running / searching worlds, [2, 8) the sync-free tail's lagged counts, [8, 10) the concurrent
+    // restoration's published list lengths): kernels store them, the host reads them after an
+    // event or a synchronised round (no fill or copy per round)
     HIPCK(hipHostMalloc((void**)&p->h_flags, 12 * sizeof(int), hipHostMallocMapped));
     HIPCK(hipHostGetDevicePointer((void**)&d.flags, p->h_flags, 0));
     // active-world lists: two per iteration (ping-pong), two per line-search round
